@@ -1,0 +1,170 @@
+/*
+ * socp.h — C ABI of libsocp, the MI355X-native batched dense SOCP solver.
+ *
+ * This is the drop-in boundary for the dense path of BenChung/Socp.jl.
+ * The reference has no C ABI of its own: its plugin interface is Julia multiple
+ * dispatch (abstract type KKTSolver{T}, Socp.jl:77-78) and the per-iteration
+ * calls compute_scaling / setup_iter / solve_kkt made by solve_socp
+ * (solver.jl:105-151).  Every entry point below names the reference interface
+ * it replaces; INTEGRATION.md shows the `ccall` binding a Julia maintainer adds.
+ *
+ * Problem (reference Socp.jl:20-38, README.md:4):
+ *     minimize c'x   s.t.  A x = b,   G x + s = h,   s in K
+ * K is a product of cones listed POC-first then SOC, contiguous over 0..k-1
+ * (scalings.jl:102).  All arithmetic is IEEE fp64.
+ *
+ * Layout (shared by host and device pointers):
+ *   - one cone description for the whole batch (every problem has the same
+ *     dims and cone structure, as the reference's Problem{C,n,m,k} type does);
+ *   - per problem, matrices are dense COLUMN-MAJOR (Julia order):
+ *       A: m x n  -> A[p*m*n + j*m + i] = A_p(i,j)
+ *       G: k x n  -> G[p*k*n + j*k + i] = G_p(i,j)
+ *     vectors are stacked batch-major: c[p*n + j], b[p*m + i], h[p*k + i], ...
+ *
+ * Errors: every function returns 0 on success and a negative SOCP_E* code on
+ * an API error; socp_last_error() gives a message (thread-local).  Numerical
+ * failures are NOT API errors: they are reported per problem in status[]
+ * (the reference instead throws PosDefException / DomainError and aborts the
+ * solve: densesolver.jl:47,51; Julia sqrt of a negative argument).
+ */
+#ifndef SOCP_H
+#define SOCP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes (API errors) ---- */
+#define SOCP_OK 0
+#define SOCP_E_INVALID (-1)     /* bad argument / shape (reference: AssertionError, Socp.jl:43-47) */
+#define SOCP_E_UNSUPPORTED (-2) /* dims not covered by any compiled kernel                          */
+#define SOCP_E_HIP (-3)         /* HIP runtime error                                                 */
+#define SOCP_E_NOMEM (-4)       /* device allocation failed                                          */
+
+/* ---- per-problem status (numerical outcome) ---- */
+#define SOCP_CONVERGED 0      /* exit test ||rd||+||rp||+z's < tol met (solver.jl:122)               */
+#define SOCP_MAXIT 1          /* iteration cap reached (solver.jl:105)                               */
+#define SOCP_CHOL_H_FAILED 2  /* H = G'W^-2G (+A'A) not positive definite (densesolver.jl:47)        */
+#define SOCP_CHOL_S_FAILED 3  /* S = A H^-1 A' not positive definite (densesolver.jl:51)            */
+#define SOCP_DOMAIN_ERROR 4   /* sqrt of a negative number: Julia throws DomainError (scalings.jl:46,47,57,68,91; mats.jl:71) */
+
+/* ---- cone kinds (reference Socp.jl:8-16) ---- */
+#define SOCP_CONE_POC 0 /* nonnegative orthant, POC{D}(offs) */
+#define SOCP_CONE_SOC 1 /* second-order cone,   SOC{D}(offs) */
+
+typedef struct socp_dims {
+  int64_t batch; /* number of independent problems B                    */
+  int32_t n;     /* variables        (Problem.n, Socp.jl:36)             */
+  int32_t m;     /* equality rows    (Problem.m)                         */
+  int32_t k;     /* cone rows        (Problem.k)                         */
+  int32_t ncones;
+} socp_dims;
+
+/* Solver constants.  Defaults (socp_params_default) equal the reference's
+ * hard-coded values: maxit 40 (solver.jl:105), tol 1e-5 absolute (:122),
+ * step 0.99 (:146), sigma exponent 3 (:133), init shift threshold 1e-10 (:91,97). */
+typedef struct socp_params {
+  int32_t maxit;
+  int32_t sigma_exp;
+  double tol;      /* tol = 0 gives the fixed-iteration ("fixed-K") mode        */
+  double step;
+  double init_eps;
+  int32_t flags;   /* SOCP_F_* bit set */
+  int32_t reserved;
+} socp_params;
+
+#define SOCP_F_DEVICE_PTRS 1 /* all data pointers are device (HBM) pointers */
+#define SOCP_F_WARM_START 2  /* x,y,z,s hold the starting iterate: skip the init solve (solver.jl:68-104) */
+
+typedef struct socp_ctx socp_ctx;
+
+/* Library / context.  One context per host thread, each owning a HIP stream
+ * (the reference indexes CHOLMOD state by Threads.threadid(), cholutils.jl:73). */
+const char* socp_last_error(void);
+const char* socp_version(void);
+void socp_params_default(socp_params* p);
+int socp_ctx_create(int device, socp_ctx** out);
+int socp_ctx_destroy(socp_ctx* ctx);
+int socp_ctx_sync(socp_ctx* ctx);
+/* hipStream_t of the context (as void*) so callers can order their own work. */
+void* socp_ctx_stream(socp_ctx* ctx);
+
+/* Largest (n, m, k) the register-resident kernel accepts; other shapes return
+ * SOCP_E_UNSUPPORTED from socp_batch_solve. */
+int socp_supported(const socp_dims* dims);
+
+/* Batched solve: replaces solve_socp(prob, SolverState(prob, DenseSolver(prob)))
+ * (solver.jl:40-153 with the DenseSolver plugin, densesolver.jl:1-90), run once
+ * per problem of the batch.
+ *   cone_kind/offs/dim : ncones entries (POC first, then SOC), host pointers.
+ *   c,A,b,G,h          : problem data (layout above).
+ *   sing               : per-problem flag; 1 if cholesky(G'G) fails (Socp.jl:49-56).
+ *                        NULL -> computed on device by the same positive-definiteness
+ *                        test the kernel uses for H.
+ *   x,y,z,s            : out (in as well with SOCP_F_WARM_START): final iterate
+ *                        (the reference returns State(x,y,z,s), solver.jl:152).
+ *   iters, status      : out, per problem (int32); iters = completed Newton steps.
+ * With SOCP_F_DEVICE_PTRS the call is stream-ordered and returns without
+ * synchronising; otherwise it copies, solves and synchronises. */
+int socp_batch_solve(socp_ctx* ctx, const socp_dims* dims,
+                     const int32_t* cone_kind, const int32_t* cone_offs, const int32_t* cone_dim,
+                     const double* c, const double* A, const double* b,
+                     const double* G, const double* h, const uint8_t* sing,
+                     const socp_params* params,
+                     double* x, double* y, double* z, double* s,
+                     int32_t* iters, int32_t* status);
+
+/* Same, plus per-problem final residual norms: res[3*p+0]=||rd||, [1]=||rp||, [2]=z's
+ * (the quantities of the exit test, solver.jl:109-122), evaluated at the returned iterate. */
+int socp_batch_solve_ex(socp_ctx* ctx, const socp_dims* dims,
+                        const int32_t* cone_kind, const int32_t* cone_offs, const int32_t* cone_dim,
+                        const double* c, const double* A, const double* b,
+                        const double* G, const double* h, const uint8_t* sing,
+                        const socp_params* params,
+                        double* x, double* y, double* z, double* s,
+                        int32_t* iters, int32_t* status, double* res);
+
+/* Single-problem plugin entries.  They replace the two KKTSolver methods of
+ * DenseSolver so the reference's own KKT golden (runtests.jl:95-128) runs
+ * through the HIP path:
+ *   setup_iter(ss::DenseSolver, pr, state, scaling)   densesolver.jl:41-52
+ *   solve_kkt (ss::DenseSolver, pr, state, scaling, dx,dy,dz,ds, cx,cy,cz,cs)   densesolver.jl:54-90
+ * Here both happen in one device call on a batch: given the iterate (s,z) the
+ * NT scaling is computed (scalings.jl:101-110), the KKT matrix factored, and the
+ * system solved for the right-hand side (dx,dy,dz,ds) -> (cx,cy,cz,cs).
+ * kkt_status[p]: 0 ok, SOCP_CHOL_H_FAILED, SOCP_CHOL_S_FAILED, SOCP_DOMAIN_ERROR. */
+int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims,
+                         const int32_t* cone_kind, const int32_t* cone_offs, const int32_t* cone_dim,
+                         const double* A, const double* G, const uint8_t* sing,
+                         const double* s, const double* z,
+                         const double* dx, const double* dy, const double* dz, const double* ds,
+                         double* cx, double* cy, double* cz, double* cs,
+                         int32_t* kkt_status, int32_t flags);
+
+/* Device-side deterministic generator of feasible synthetic problems
+ * (SURVEY.md §8(d)): counter-based SplitMix64 keyed on the GLOBAL problem
+ * index first_problem + p, so shards of a multi-GPU run reproduce the same
+ * problems.  Output pointers are device pointers with the layout above. */
+int socp_generate(socp_ctx* ctx, const socp_dims* dims,
+                  const int32_t* cone_kind, const int32_t* cone_offs, const int32_t* cone_dim,
+                  uint64_t seed, int64_t first_problem,
+                  double* c, double* A, double* b, double* G, double* h);
+
+/* Timing of the last solve's main kernel, measured with HIP events on the
+ * context's stream (milliseconds), and its name. */
+int socp_last_kernel_ms(socp_ctx* ctx, float* ms);
+const char* socp_last_kernel_name(socp_ctx* ctx);
+
+/* Testing hook (not part of the reference surface): when set to a device buffer
+ * of batch*(2n^2+2k) doubles, socp_batch_kkt_solve dumps per problem the KKT
+ * matrix H = G'W^-2G (+A'A) (densesolver.jl:43-46), its inverse Li (:48),
+ * lambda and wbar (scalings.jl:1-20).  NULL disables. */
+int socp_debug_set_kkt_dump(double* dev_buf);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SOCP_H */

@@ -1,0 +1,520 @@
+// socp_api.hip — C ABI of libsocp (include/socp.h): contexts, device buffers,
+// variant dispatch for the register-resident solver kernel, the device-side
+// problem generator.  Host pointers are staged through context-owned device
+// buffers; device pointers (SOCP_F_DEVICE_PTRS) are used in place.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/socp.h"
+#include "socp_kernels.hpp"
+
+using namespace socp;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess)                                                           \
+      return fail(SOCP_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_));      \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes < 256 ? 256 : bytes;
+    if (hipMalloc(&p, want) != hipSuccess) return SOCP_E_NOMEM;
+    cap = want;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct socp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int num_cu = 0;
+  float last_ms = 0.f;
+  const char* last_name = "";
+  enum { B_C, B_A, B_B, B_G, B_H, B_SING, B_X, B_Y, B_Z, B_S, B_IT, B_ST, B_RES, B_DX, B_DY,
+         B_DZ, B_DS, B_CX, B_CY, B_CZ, B_CS, B_CNT, NB };
+  DevBuf buf[NB];
+};
+
+extern "C" const char* socp_last_error(void) { return g_err.c_str(); }
+extern "C" const char* socp_version(void) { return "socp-mi355x 0.1 (gfx950)"; }
+
+extern "C" void socp_params_default(socp_params* p) {
+  p->maxit = 40;
+  p->sigma_exp = 3;
+  p->tol = 1e-5;
+  p->step = 0.99;
+  p->init_eps = 1e-10;
+  p->flags = 0;
+  p->reserved = 0;
+}
+
+extern "C" int socp_ctx_create(int device, socp_ctx** out) {
+  if (!out) return fail(SOCP_E_INVALID, "out is NULL");
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(SOCP_E_INVALID, "bad device index");
+  HIPCHK(hipSetDevice(device));
+  socp_ctx* c = new socp_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  c->num_cu = prop.multiProcessorCount;
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&c->ev0));
+  HIPCHK(hipEventCreate(&c->ev1));
+  *out = c;
+  return 0;
+}
+
+extern "C" int socp_ctx_destroy(socp_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& b : c->buf) b.release();
+  (void)hipEventDestroy(c->ev0);
+  (void)hipEventDestroy(c->ev1);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+extern "C" int socp_ctx_sync(socp_ctx* c) {
+  if (!c) return fail(SOCP_E_INVALID, "ctx is NULL");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+extern "C" void* socp_ctx_stream(socp_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+extern "C" int socp_last_kernel_ms(socp_ctx* c, float* ms) {
+  if (!c || !ms) return fail(SOCP_E_INVALID, "NULL argument");
+  HIPCHK(hipEventSynchronize(c->ev1));
+  HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  *ms = c->last_ms;
+  return 0;
+}
+extern "C" const char* socp_last_kernel_name(socp_ctx* c) { return c ? c->last_name : ""; }
+
+// ---------------------------------------------------------------- checks
+static int check_problem(const socp_dims* d, const int32_t* kind, const int32_t* offs,
+                         const int32_t* dim, ConeTable* tab, int* degree) {
+  if (!d) return fail(SOCP_E_INVALID, "dims is NULL");
+  if (d->batch < 0 || d->n <= 0 || d->m < 0 || d->k <= 0 || d->ncones <= 0)
+    return fail(SOCP_E_INVALID, "bad dims (need batch>=0, n>0, m>=0, k>0, ncones>0)");
+  if (d->ncones > MAXC) return fail(SOCP_E_UNSUPPORTED, "too many cones");
+  if (!kind || !offs || !dim) return fail(SOCP_E_INVALID, "cone arrays are NULL");
+  int next = 0, deg = 0;
+  bool seen_soc = false;
+  tab->nc = d->ncones;
+  for (int c = 0; c < d->ncones; ++c) {
+    if (kind[c] != SOCP_CONE_POC && kind[c] != SOCP_CONE_SOC)
+      return fail(SOCP_E_INVALID, "cone kind must be POC(0) or SOC(1)");
+    if (offs[c] != next || dim[c] <= 0)
+      return fail(SOCP_E_INVALID, "cones must be contiguous from 0 with dim>0 (scalings.jl:102)");
+    if (kind[c] == SOCP_CONE_POC && seen_soc)
+      return fail(SOCP_E_INVALID, "cones must list POC before SOC (scalings.jl:102)");
+    if (kind[c] == SOCP_CONE_SOC) seen_soc = true;
+    tab->kind[c] = kind[c];
+    tab->offs[c] = offs[c];
+    tab->dim[c] = dim[c];
+    next += dim[c];
+    deg += (kind[c] == SOCP_CONE_POC) ? dim[c] : 1;
+  }
+  if (next != d->k) return fail(SOCP_E_INVALID, "cone dims must sum to k");
+  *degree = deg;
+  return 0;
+}
+
+static const SmallVariant* pick_variant(int n, int m, int k) {
+  int cnt = 0;
+  const SmallVariant* v = small_variants(&cnt);
+  const SmallVariant* best = nullptr;
+  long best_cost = 0;
+  for (int i = 0; i < cnt; ++i) {
+    if (16 * v[i].NQ < n || 4 * v[i].NP < k || 16 * v[i].MQ < (m > 0 ? m : 1)) continue;
+    if (k > KMAX) continue;
+    long cost = (long)v[i].NQ * v[i].NQ * v[i].NP * 64 + (long)v[i].MQ * 16;
+    if (!best || cost < best_cost) {
+      best = &v[i];
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
+extern "C" int socp_supported(const socp_dims* d) {
+  if (!d) return 0;
+  return pick_variant(d->n, d->m, d->k) != nullptr && d->ncones <= NCS;
+}
+
+// ---------------------------------------------------------------- launch
+static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
+  size_t lds = small_lds_bytes(v->NQ, v->NP, v->MQ);
+  if (lds > 160 * 1024) return fail(SOCP_E_UNSUPPORTED, "LDS footprint too large");
+  if (lds > 64 * 1024)
+    HIPCHK(hipFuncSetAttribute(v->kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v->kernel, 64, lds));
+  if (per_cu < 1) per_cu = 1;
+  int64_t blocks = (int64_t)ctx->num_cu * per_cu;
+  if (blocks > args.B) blocks = args.B;
+  if (blocks < 1) blocks = 1;
+  HIPCHK(hipMemsetAsync(args.counter, 0, sizeof(int32_t), ctx->stream));
+  void* kargs[] = {&args};
+  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIPCHK(hipLaunchKernel(v->kernel, dim3((unsigned)blocks), dim3(64), kargs, lds, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  ctx->last_name = v->name;
+  return 0;
+}
+
+template <class T>
+static int stage_in(socp_ctx* ctx, int slot, const T* src, size_t count, bool dev, const T** out) {
+  if (!src || count == 0) {
+    *out = src;
+    return 0;
+  }
+  if (dev) {
+    *out = src;
+    return 0;
+  }
+  int rc = ctx->buf[slot].ensure(count * sizeof(T));
+  if (rc) return fail(rc, "device allocation failed");
+  HIPCHK(hipMemcpyAsync(ctx->buf[slot].p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  *out = (const T*)ctx->buf[slot].p;
+  return 0;
+}
+template <class T>
+static int stage_out(socp_ctx* ctx, int slot, T* user, size_t count, bool dev, bool copy_in,
+                     T** out) {
+  if (!user || count == 0) {
+    *out = user;
+    return 0;
+  }
+  if (dev) {
+    *out = user;
+    return 0;
+  }
+  int rc = ctx->buf[slot].ensure(count * sizeof(T));
+  if (rc) return fail(rc, "device allocation failed");
+  if (copy_in)
+    HIPCHK(hipMemcpyAsync(ctx->buf[slot].p, user, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+  *out = (T*)ctx->buf[slot].p;
+  return 0;
+}
+template <class T>
+static int copy_back(socp_ctx* ctx, T* user, const T* devp, size_t count, bool dev) {
+  if (dev || !user || count == 0) return 0;
+  HIPCHK(hipMemcpyAsync(user, devp, count * sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
+  return 0;
+}
+
+#define TRY(x)          \
+  do {                  \
+    int rc_ = (x);      \
+    if (rc_) return rc_; \
+  } while (0)
+
+extern "C" int socp_batch_solve_ex(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,
+                                   const int32_t* cone_offs, const int32_t* cone_dim,
+                                   const double* c, const double* A, const double* b,
+                                   const double* G, const double* h, const uint8_t* sing,
+                                   const socp_params* params, double* x, double* y, double* z,
+                                   double* s, int32_t* iters, int32_t* status, double* res) {
+  if (!ctx) return fail(SOCP_E_INVALID, "ctx is NULL");
+  SmallArgs a;
+  memset(&a, 0, sizeof(a));
+  int degree = 0;
+  TRY(check_problem(dims, cone_kind, cone_offs, cone_dim, &a.cones, &degree));
+  socp_params P;
+  if (params)
+    P = *params;
+  else
+    socp_params_default(&P);
+  const int64_t B = dims->batch;
+  const int n = dims->n, m = dims->m, k = dims->k;
+  if (B == 0) return 0;
+  if (!c || !G || !h || !x || !z || !s || !iters || !status || (m > 0 && (!A || !b || !y)))
+    return fail(SOCP_E_INVALID, "NULL data pointer");
+  const SmallVariant* v = pick_variant(n, m, k);
+  if (!v || dims->ncones > NCS)
+    return fail(SOCP_E_UNSUPPORTED, "dims outside the register-resident kernel (n<=64, m<=64, k<=128, <=8 cones)");
+  HIPCHK(hipSetDevice(ctx->device));
+  const bool dev = (P.flags & SOCP_F_DEVICE_PTRS) != 0;
+  const bool warm = (P.flags & SOCP_F_WARM_START) != 0;
+  a.B = B;
+  a.n = n;
+  a.m = m;
+  a.k = k;
+  a.nc = dims->ncones;
+  a.maxit = P.maxit;
+  a.sigma_exp = P.sigma_exp;
+  a.tol = P.tol;
+  a.step = P.step;
+  a.init_eps = P.init_eps;
+  a.flags = P.flags;
+  a.mode = MODE_SOLVE;
+  a.deg = degree;
+  typedef socp_ctx X;
+  TRY(stage_in(ctx, X::B_C, c, (size_t)B * n, dev, &a.c));
+  TRY(stage_in(ctx, X::B_A, A, (size_t)B * m * n, dev, &a.A));
+  TRY(stage_in(ctx, X::B_B, b, (size_t)B * m, dev, &a.b));
+  TRY(stage_in(ctx, X::B_G, G, (size_t)B * k * n, dev, &a.G));
+  TRY(stage_in(ctx, X::B_H, h, (size_t)B * k, dev, &a.h));
+  TRY(stage_in(ctx, X::B_SING, sing, (size_t)B, dev, &a.sing));
+  TRY(stage_out(ctx, X::B_X, x, (size_t)B * n, dev, warm, &a.x));
+  TRY(stage_out(ctx, X::B_Y, y, (size_t)B * m, dev, warm, &a.y));
+  TRY(stage_out(ctx, X::B_Z, z, (size_t)B * k, dev, warm, &a.z));
+  TRY(stage_out(ctx, X::B_S, s, (size_t)B * k, dev, warm, &a.s));
+  TRY(stage_out(ctx, X::B_IT, iters, (size_t)B, dev, false, &a.iters));
+  TRY(stage_out(ctx, X::B_ST, status, (size_t)B, dev, false, &a.status));
+  TRY(stage_out(ctx, X::B_RES, res, (size_t)B * 3, dev, false, &a.res));
+  if (ctx->buf[X::B_CNT].ensure(256)) return fail(SOCP_E_NOMEM, "device allocation failed");
+  a.counter = (int32_t*)ctx->buf[X::B_CNT].p;
+  TRY(launch_small(ctx, a, v));
+  TRY(copy_back(ctx, x, a.x, (size_t)B * n, dev));
+  TRY(copy_back(ctx, y, a.y, (size_t)B * m, dev));
+  TRY(copy_back(ctx, z, a.z, (size_t)B * k, dev));
+  TRY(copy_back(ctx, s, a.s, (size_t)B * k, dev));
+  TRY(copy_back(ctx, iters, a.iters, (size_t)B, dev));
+  TRY(copy_back(ctx, status, a.status, (size_t)B, dev));
+  TRY(copy_back(ctx, res, a.res, (size_t)B * 3, dev));
+  if (!dev) HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+extern "C" int socp_batch_solve(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,
+                                const int32_t* cone_offs, const int32_t* cone_dim, const double* c,
+                                const double* A, const double* b, const double* G, const double* h,
+                                const uint8_t* sing, const socp_params* params, double* x,
+                                double* y, double* z, double* s, int32_t* iters, int32_t* status) {
+  return socp_batch_solve_ex(ctx, dims, cone_kind, cone_offs, cone_dim, c, A, b, G, h, sing, params,
+                             x, y, z, s, iters, status, nullptr);
+}
+
+static double* g_kkt_debug = nullptr;  // device buffer for socp_debug_kkt (testing hook)
+
+extern "C" int socp_debug_set_kkt_dump(double* dev_buf) {
+  g_kkt_debug = dev_buf;
+  return 0;
+}
+
+extern "C" int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,
+                                    const int32_t* cone_offs, const int32_t* cone_dim,
+                                    const double* A, const double* G, const uint8_t* sing,
+                                    const double* s, const double* z, const double* dx,
+                                    const double* dy, const double* dz, const double* ds,
+                                    double* cx, double* cy, double* cz, double* cs,
+                                    int32_t* kkt_status, int32_t flags) {
+  if (!ctx) return fail(SOCP_E_INVALID, "ctx is NULL");
+  SmallArgs a;
+  memset(&a, 0, sizeof(a));
+  int degree = 0;
+  TRY(check_problem(dims, cone_kind, cone_offs, cone_dim, &a.cones, &degree));
+  const int64_t B = dims->batch;
+  const int n = dims->n, m = dims->m, k = dims->k;
+  if (B == 0) return 0;
+  if (!G || !s || !z || !dx || !dz || !ds || !cx || !cz || !cs || !kkt_status ||
+      (m > 0 && (!A || !dy || !cy)))
+    return fail(SOCP_E_INVALID, "NULL data pointer");
+  const SmallVariant* v = pick_variant(n, m, k);
+  if (!v || dims->ncones > NCS) return fail(SOCP_E_UNSUPPORTED, "dims outside the register-resident kernel");
+  HIPCHK(hipSetDevice(ctx->device));
+  const bool dev = (flags & SOCP_F_DEVICE_PTRS) != 0;
+  a.B = B;
+  a.n = n;
+  a.m = m;
+  a.k = k;
+  a.nc = dims->ncones;
+  a.mode = MODE_KKT;
+  a.deg = degree;
+  a.dbg = g_kkt_debug;
+  a.maxit = 1;
+  a.sigma_exp = 3;
+  typedef socp_ctx X;
+  // c, b, h are not used by the KKT entry but the loader reads them: point at zeros
+  if (ctx->buf[X::B_C].ensure((size_t)B * (n + m + k) * sizeof(double))) return fail(SOCP_E_NOMEM, "alloc");
+  HIPCHK(hipMemsetAsync(ctx->buf[X::B_C].p, 0, (size_t)B * (n + m + k) * sizeof(double), ctx->stream));
+  a.c = (const double*)ctx->buf[X::B_C].p;
+  a.b = a.c + (size_t)B * n;
+  a.h = a.b + (size_t)B * m;
+  TRY(stage_in(ctx, X::B_A, A, (size_t)B * m * n, dev, &a.A));
+  TRY(stage_in(ctx, X::B_G, G, (size_t)B * k * n, dev, &a.G));
+  TRY(stage_in(ctx, X::B_SING, sing, (size_t)B, dev, &a.sing));
+  TRY(stage_out(ctx, X::B_S, const_cast<double*>(s), (size_t)B * k, dev, true, &a.s));
+  TRY(stage_out(ctx, X::B_Z, const_cast<double*>(z), (size_t)B * k, dev, true, &a.z));
+  TRY(stage_in(ctx, X::B_DX, dx, (size_t)B * n, dev, &a.dx));
+  TRY(stage_in(ctx, X::B_DY, dy, (size_t)B * m, dev, &a.dy));
+  TRY(stage_in(ctx, X::B_DZ, dz, (size_t)B * k, dev, &a.dz));
+  TRY(stage_in(ctx, X::B_DS, ds, (size_t)B * k, dev, &a.ds));
+  TRY(stage_out(ctx, X::B_CX, cx, (size_t)B * n, dev, false, &a.cx));
+  TRY(stage_out(ctx, X::B_CY, cy, (size_t)B * m, dev, false, &a.cy));
+  TRY(stage_out(ctx, X::B_CZ, cz, (size_t)B * k, dev, false, &a.cz));
+  TRY(stage_out(ctx, X::B_CS, cs, (size_t)B * k, dev, false, &a.cs));
+  TRY(stage_out(ctx, X::B_ST, kkt_status, (size_t)B, dev, false, &a.status));
+  if (ctx->buf[X::B_CNT].ensure(256)) return fail(SOCP_E_NOMEM, "device allocation failed");
+  a.counter = (int32_t*)ctx->buf[X::B_CNT].p;
+  TRY(launch_small(ctx, a, v));
+  TRY(copy_back(ctx, cx, a.cx, (size_t)B * n, dev));
+  TRY(copy_back(ctx, cy, a.cy, (size_t)B * m, dev));
+  TRY(copy_back(ctx, cz, a.cz, (size_t)B * k, dev));
+  TRY(copy_back(ctx, cs, a.cs, (size_t)B * k, dev));
+  TRY(copy_back(ctx, kkt_status, a.status, (size_t)B, dev));
+  if (!dev) HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+// ------------------------------------------------------------- generator
+// u = splitmix64(seed ^ (p<<24 | e)), U = (u>>11)*2^-53,
+// p the GLOBAL problem index.  Sequential sums without FMA contraction so the
+// CPU restatement (oracle/socp_oracle.c: or_generate) is bit-identical.
+namespace {
+struct GenArgs {
+  int64_t B, first;
+  uint64_t seed;
+  int32_t n, m, k, nc;
+  double *c, *A, *b, *G, *h;
+  ConeTable cones;
+};
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ double gen_u(uint64_t seed, uint64_t p, uint64_t e) {
+  uint64_t u = splitmix64(seed ^ ((p << 24) | e));
+  return __dmul_rn((double)(u >> 11), 0x1.0p-53);
+}
+__device__ __forceinline__ double gen_sym(uint64_t seed, uint64_t p, uint64_t e) {
+  return __dsub_rn(__dmul_rn(2.0, gen_u(seed, p, e)), 1.0);
+}
+
+__global__ void __launch_bounds__(256) socp_generate_kernel(GenArgs a) {
+  extern __shared__ double sh[];
+  const int64_t p = blockIdx.x;
+  const uint64_t gp = (uint64_t)(a.first + p);
+  const int n = a.n, m = a.m, k = a.k;
+  double* x0 = sh;
+  double* y0 = x0 + n;
+  double* s0 = y0 + m;
+  double* z0 = s0 + k;
+  const uint64_t kn = (uint64_t)k * n, mn = (uint64_t)m * n;
+  double* Gp = a.G + p * (int64_t)kn;
+  double* Ap = a.A + p * (int64_t)mn;
+  for (uint64_t e = threadIdx.x; e < kn; e += blockDim.x) Gp[e] = gen_sym(a.seed, gp, e);
+  for (uint64_t e = threadIdx.x; e < mn; e += blockDim.x) Ap[e] = gen_sym(a.seed, gp, kn + e);
+  const uint64_t base = kn + mn;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) x0[j] = gen_sym(a.seed, gp, base + j);
+  for (int i = threadIdx.x; i < m; i += blockDim.x) y0[i] = gen_sym(a.seed, gp, base + n + i);
+  const uint64_t base2 = base + n + m;
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    int c = 0;
+    while (!(i >= a.cones.offs[c] && i < a.cones.offs[c] + a.cones.dim[c])) ++c;
+    const int o = a.cones.offs[c], d = a.cones.dim[c];
+    const uint64_t es = base2 + 2 * (uint64_t)o, ez = es + d;
+    if (a.cones.kind[c] == POC_K) {
+      s0[i] = __dadd_rn(0.5, gen_u(a.seed, gp, es + (i - o)));
+      z0[i] = __dadd_rn(0.5, gen_u(a.seed, gp, ez + (i - o)));
+    } else if (i > o) {
+      s0[i] = gen_sym(a.seed, gp, es + (i - o - 1));
+      z0[i] = gen_sym(a.seed, gp, ez + (i - o - 1));
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.nc; c += blockDim.x) {
+    if (a.cones.kind[c] != SOC_K) continue;
+    const int o = a.cones.offs[c], d = a.cones.dim[c];
+    const uint64_t es = base2 + 2 * (uint64_t)o, ez = es + d;
+    double qs = 0.0, qz = 0.0;
+    for (int i = 1; i < d; ++i) {
+      qs = __dadd_rn(qs, __dmul_rn(s0[o + i], s0[o + i]));
+      qz = __dadd_rn(qz, __dmul_rn(z0[o + i], z0[o + i]));
+    }
+    s0[o] = __dadd_rn(__dadd_rn(__dsqrt_rn(qs), 0.5), gen_u(a.seed, gp, es + d - 1));
+    z0[o] = __dadd_rn(__dadd_rn(__dsqrt_rn(qz), 0.5), gen_u(a.seed, gp, ez + d - 1));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    double acc = 0.0;
+    for (int j = 0; j < n; ++j)
+      acc = __dadd_rn(acc, __dmul_rn(gen_sym(a.seed, gp, (uint64_t)j * k + i), x0[j]));
+    a.h[p * k + i] = __dadd_rn(acc, s0[i]);
+  }
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    double acc = 0.0;
+    for (int j = 0; j < n; ++j)
+      acc = __dadd_rn(acc, __dmul_rn(gen_sym(a.seed, gp, kn + (uint64_t)j * m + i), x0[j]));
+    a.b[p * m + i] = acc;
+  }
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    double t = 0.0, u = 0.0;
+    for (int i = 0; i < m; ++i)
+      t = __dadd_rn(t, __dmul_rn(gen_sym(a.seed, gp, kn + (uint64_t)j * m + i), y0[i]));
+    for (int i = 0; i < k; ++i)
+      u = __dadd_rn(u, __dmul_rn(gen_sym(a.seed, gp, (uint64_t)j * k + i), z0[i]));
+    a.c[p * n + j] = -__dadd_rn(t, u);
+  }
+}
+}  // namespace
+
+extern "C" int socp_generate(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,
+                             const int32_t* cone_offs, const int32_t* cone_dim, uint64_t seed,
+                             int64_t first_problem, double* c, double* A, double* b, double* G,
+                             double* h) {
+  if (!ctx) return fail(SOCP_E_INVALID, "ctx is NULL");
+  GenArgs a;
+  memset(&a, 0, sizeof(a));
+  int degree = 0;
+  TRY(check_problem(dims, cone_kind, cone_offs, cone_dim, &a.cones, &degree));
+  if (dims->batch == 0) return 0;
+  if (!c || !G || !h || (dims->m > 0 && (!A || !b))) return fail(SOCP_E_INVALID, "NULL data pointer");
+  if ((uint64_t)dims->k * dims->n + (uint64_t)dims->m * dims->n + dims->n + dims->m + 2 * dims->k >= (1ull << 24))
+    return fail(SOCP_E_UNSUPPORTED, "problem too large for the 24-bit element counter");
+  HIPCHK(hipSetDevice(ctx->device));
+  a.B = dims->batch;
+  a.first = first_problem;
+  a.seed = seed;
+  a.n = dims->n;
+  a.m = dims->m;
+  a.k = dims->k;
+  a.nc = dims->ncones;
+  a.c = c;
+  a.A = A;
+  a.b = b;
+  a.G = G;
+  a.h = h;
+  size_t sh = sizeof(double) * (size_t)(a.n + a.m + 2 * a.k);
+  if (sh > 64 * 1024) return fail(SOCP_E_UNSUPPORTED, "generator LDS too large");
+  void* kargs[] = {&a};
+  HIPCHK(hipLaunchKernel((const void*)&socp_generate_kernel, dim3((unsigned)a.B), dim3(256), kargs,
+                         sh, ctx->stream));
+  return 0;
+}

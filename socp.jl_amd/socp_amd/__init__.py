@@ -1,0 +1,345 @@
+"""socp_amd — MI355X-native batched dense SOCP solver (host side).
+
+Two layers over libsocp.so (include/socp.h):
+
+* ``batch_solve`` / ``batch_kkt_solve`` / ``generate``: the batched C-ABI
+  entry points, taking numpy arrays (host) or torch CUDA tensors (device).
+* A mirror of the reference Julia surface for the dense path
+  (BenChung/Socp.jl): ``POC``, ``SOC`` (Socp.jl:9-16), ``Problem``
+  (Socp.jl:20-60), ``State`` (Socp.jl:62-75), ``DenseSolver`` (the
+  KKTSolver plugin, densesolver.jl:1-90, here running on the GPU),
+  ``SolverState`` (solver.jl:1-38), ``solve_socp`` (solver.jl:40-153),
+  ``compute_scaling`` / ``setup_iter`` / ``solve_kkt`` with the reference's
+  argument meaning and error behaviour (PosDefException from cholesky!,
+  DomainError from sqrt of a negative number, AssertionError on shapes).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._lib import (CHOL_H_FAILED, CHOL_S_FAILED, CONE_POC, CONE_SOC, CONVERGED, DOMAIN_ERROR,
+                   F_DEVICE_PTRS, F_WARM_START, MAXIT, Context, SocpError, default_context,
+                   default_params)
+
+__all__ = [
+    "POC", "SOC", "Problem", "State", "Scaling", "DenseSolver", "HipDenseSolver", "SolverState",
+    "solve_socp", "solve_socp_batched", "compute_scaling", "setup_iter", "solve_kkt",
+    "PosDefException", "DomainError", "batch_solve", "batch_kkt_solve", "generate",
+    "Context", "SocpError", "default_context", "cone_arrays",
+    "CONVERGED", "MAXIT", "CHOL_H_FAILED", "CHOL_S_FAILED", "DOMAIN_ERROR",
+]
+
+STATUS_NAMES = {CONVERGED: "converged", MAXIT: "maxit", CHOL_H_FAILED: "chol(H) failed",
+                CHOL_S_FAILED: "chol(S) failed", DOMAIN_ERROR: "domain error"}
+
+
+class PosDefException(Exception):
+    """Raised where the reference's cholesky! throws (densesolver.jl:47,51)."""
+
+
+class DomainError(Exception):
+    """Raised where the reference's sqrt of a negative number throws."""
+
+
+# ----------------------------------------------------------------- cones
+class POC:
+    """Nonnegative orthant cone POC(offs, dim) (Socp.jl:9-12)."""
+
+    kind = CONE_POC
+
+    def __init__(self, offs: int, dim: int):
+        self.offs, self.dim = int(offs), int(dim)
+
+    def __repr__(self):
+        return f"POC({self.offs},{self.dim})"
+
+
+class SOC:
+    """Second-order cone SOC(offs, dim) (Socp.jl:13-16)."""
+
+    kind = CONE_SOC
+
+    def __init__(self, offs: int, dim: int):
+        self.offs, self.dim = int(offs), int(dim)
+
+    def __repr__(self):
+        return f"SOC({self.offs},{self.dim})"
+
+
+def _as_cone_list(cones):
+    out = []
+    for c in cones:
+        if isinstance(c, (POC, SOC)):
+            out.append((c.kind, c.offs, c.dim))
+        else:
+            out.append((int(c[0]), int(c[1]), int(c[2])))
+    return out
+
+
+def cone_arrays(cones):
+    cl = _as_cone_list(cones)
+    kind = np.array([c[0] for c in cl], dtype=np.int32)
+    offs = np.array([c[1] for c in cl], dtype=np.int32)
+    dim = np.array([c[2] for c in cl], dtype=np.int32)
+    return kind, offs, dim
+
+
+# --------------------------------------------------------------- batched
+def _is_torch(a):
+    return a is not None and not isinstance(a, np.ndarray) and hasattr(a, "data_ptr")
+
+
+def _host(a, dtype=np.float64):
+    if a is None:
+        return None
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5, step=0.99,
+                sigma_exp=3, init_eps=1e-10, warm=None, ctx=None, res=False, out=None):
+    """Solve a batch of independent problems (same dims and cone structure).
+
+    Arrays follow include/socp.h: per-problem column-major A (m x n), G (k x n)
+    stacked batch-major, vectors stacked batch-major.  numpy inputs run through
+    host staging buffers; torch CUDA tensors are used in place (device mode,
+    stream-ordered on the context's stream; call ctx.sync() before reading).
+    Returns dict(x, y, z, s, iters, status[, res]).
+    """
+    ctx = ctx or default_context()
+    L = _lib.load()
+    kind, offs, dim = cone_arrays(cones)
+    B = (c.numel() if _is_torch(c) else np.size(c)) // n
+    dims = _lib.Dims(B, n, m, k, len(kind))
+    dev = _is_torch(G)
+    flags = F_DEVICE_PTRS if dev else 0
+    if warm is not None:
+        flags |= F_WARM_START
+    P = default_params(maxit=maxit, tol=tol, step=step, sigma_exp=sigma_exp, init_eps=init_eps,
+                       flags=flags)
+    if dev:
+        import torch
+        devc = G.device
+        if out is None:
+            f64 = dict(dtype=torch.float64, device=devc)
+            out = dict(x=torch.empty(B * n, **f64), y=torch.empty(max(B * m, 1), **f64),
+                       z=torch.empty(B * k, **f64), s=torch.empty(B * k, **f64),
+                       iters=torch.empty(B, dtype=torch.int32, device=devc),
+                       status=torch.empty(B, dtype=torch.int32, device=devc))
+            if res:
+                out["res"] = torch.empty(3 * B, **f64)
+        if warm is not None:
+            for key, v in zip("xyzs", warm):
+                if key == "y" and m == 0:
+                    continue
+                out[key].copy_(v.reshape(-1))
+        arrs = dict(c=c, A=A, b=b, G=G, h=h, sing=sing)
+    else:
+        out = dict(x=np.zeros(B * n), y=np.zeros(max(B * m, 1)), z=np.zeros(B * k),
+                   s=np.zeros(B * k), iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32))
+        if res:
+            out["res"] = np.zeros(3 * B)
+        if warm is not None:
+            for key, v in zip("xyzs", warm):
+                if key == "y" and m == 0:
+                    continue
+                out[key][:] = np.asarray(v, dtype=np.float64).reshape(-1)
+        arrs = dict(c=_host(c), A=_host(A) if m else None, b=_host(b) if m else None, G=_host(G),
+                    h=_host(h), sing=_host(sing, np.uint8) if sing is not None else None)
+    p = _lib.ptr
+    rc = L.socp_batch_solve_ex(
+        ctx.handle, dims, p(kind), p(offs), p(dim), p(arrs["c"]), p(arrs["A"] if m else None),
+        p(arrs["b"] if m else None), p(arrs["G"]), p(arrs["h"]), p(arrs["sing"]), P,
+        p(out["x"]), p(out["y"] if m else None), p(out["z"]), p(out["s"]), p(out["iters"]),
+        p(out["status"]), p(out.get("res")))
+    _lib.check(rc)
+    if not dev and m == 0:
+        out["y"] = out["y"][:0]
+    return out
+
+
+def batch_kkt_solve(cones, n, m, k, A, G, sing, s, z, dx, dy, dz, ds, *, ctx=None):
+    """One KKT solve per problem at iterate (s, z): scaling + setup_iter + solve_kkt
+    (densesolver.jl:41-90) on the GPU.  Host (numpy) arrays.  Returns dict(cx,cy,cz,cs,status)."""
+    ctx = ctx or default_context()
+    L = _lib.load()
+    kind, offs, dim = cone_arrays(cones)
+    B = np.size(s) // k
+    dims = _lib.Dims(B, n, m, k, len(kind))
+    cx, cy, cz, cs = np.zeros(B * n), np.zeros(max(B * m, 1)), np.zeros(B * k), np.zeros(B * k)
+    st = np.zeros(B, np.int32)
+    p = _lib.ptr
+    sg = None if sing is None else _host(sing, np.uint8)
+    rc = L.socp_batch_kkt_solve(ctx.handle, dims, p(kind), p(offs), p(dim),
+                                p(_host(A) if m else None), p(_host(G)), p(sg), p(_host(s)), p(_host(z)),
+                                p(_host(dx)), p(_host(dy) if m else None), p(_host(dz)), p(_host(ds)),
+                                p(cx), p(cy if m else None), p(cz), p(cs), p(st), 0)
+    _lib.check(rc)
+    return dict(cx=cx, cy=cy[:B * m], cz=cz, cs=cs, status=st)
+
+
+def generate(cones, B, n, m, k, seed, first_problem=0, *, ctx=None, device=None):
+    """Device-side generation of B feasible synthetic problems;
+    returns torch CUDA tensors (c, A, b, G, h) in the include/socp.h layout."""
+    import torch
+    ctx = ctx or default_context()
+    dev = device or torch.device("cuda", ctx.device)
+    f64 = dict(dtype=torch.float64, device=dev)
+    c, A, b = torch.empty(B * n, **f64), torch.empty(max(B * m * n, 1), **f64), torch.empty(max(B * m, 1), **f64)
+    G, h = torch.empty(B * k * n, **f64), torch.empty(B * k, **f64)
+    kind, offs, dim = cone_arrays(cones)
+    dims = _lib.Dims(B, n, m, k, len(kind))
+    p = _lib.ptr
+    _lib.check(_lib.load().socp_generate(ctx.handle, dims, p(kind), p(offs), p(dim), seed,
+                                         first_problem, p(c), p(A), p(b), p(G), p(h)))
+    return c, A[:B * m * n], b[:B * m], G, h
+
+
+# ------------------------------------------------- reference-shaped mirror
+def _colmajor(M, rows, cols):
+    M = np.asarray(M, dtype=np.float64).reshape(rows, cols) if rows * cols else np.zeros((rows, cols))
+    return np.ascontiguousarray(M.ravel(order="F"))
+
+
+class Problem:
+    """Problem(c, A, b, G, h, cones) (Socp.jl:40-59).  `sing` is true when
+    cholesky(G'G) throws, exactly the reference's rule (Socp.jl:49-56)."""
+
+    def __init__(self, c, A, b, G, h, cones):
+        c = np.asarray(c, dtype=np.float64).reshape(-1)
+        n = len(c)
+        A = np.asarray(A, dtype=np.float64)
+        A = A.reshape(-1, n) if A.size else np.zeros((0, n))
+        b = np.asarray(b, dtype=np.float64).reshape(-1)
+        G = np.asarray(G, dtype=np.float64)
+        h = np.asarray(h, dtype=np.float64).reshape(-1)
+        m = A.shape[0]
+        assert len(b) == m
+        assert A.shape[1] == n
+        assert G.shape[1] == n
+        k = G.shape[0]
+        assert len(h) == k
+        self.c, self.A, self.b, self.G, self.h = c, A, b, G, h
+        self.cones = tuple(cones)
+        self.n, self.m, self.k = n, m, k
+        try:
+            np.linalg.cholesky(G.T @ G)
+            self.sing = False
+        except np.linalg.LinAlgError:
+            self.sing = True
+
+
+class State:
+    """State(prob, x, y, z, s) (Socp.jl:62-75)."""
+
+    def __init__(self, prob: Problem, x, y, z, s):
+        self.x = np.array(x, dtype=np.float64).reshape(-1)
+        self.y = np.array(y, dtype=np.float64).reshape(-1)
+        self.z = np.array(z, dtype=np.float64).reshape(-1)
+        self.s = np.array(s, dtype=np.float64).reshape(-1)
+        assert len(self.x) == prob.n
+        assert len(self.y) == prob.m
+        assert len(self.z) == prob.k
+        assert len(self.s) == prob.k
+
+
+class Scaling:
+    """NT scaling handle (scalings.jl:1-20).  The scaling itself is computed on
+    the GPU inside each KKT call; this object records the (s, z) it is built from."""
+
+    def __init__(self, prob: Problem):
+        self.s = np.zeros(prob.k)
+        self.z = np.zeros(prob.k)
+
+
+def compute_scaling(cones, scaling: Scaling, s, z):
+    """compute_scaling(cones, scaling, s, z) (scalings.jl:101-110)."""
+    scaling.s = np.array(s, dtype=np.float64)
+    scaling.z = np.array(z, dtype=np.float64)
+    return scaling
+
+
+class DenseSolver:
+    """KKTSolver{Scaling} plugin for the dense path (densesolver.jl:1-90), on MI355X."""
+
+    scaling_type = Scaling
+
+    def __init__(self, prob: Problem, ctx: Context | None = None):
+        self.prob = prob
+        self.ctx = ctx
+        self._sz = None
+
+
+HipDenseSolver = DenseSolver
+
+
+def setup_iter(solver: DenseSolver, prob: Problem, state: State, scaling: Scaling):
+    """setup_iter(::DenseSolver, ...) (densesolver.jl:41-52): the factorisation is
+    fused with the solve on the GPU; this records the iterate it applies to."""
+    solver._sz = (scaling.s.copy(), scaling.z.copy())
+
+
+def _raise_status(st):
+    if st in (CHOL_H_FAILED, CHOL_S_FAILED):
+        raise PosDefException(STATUS_NAMES[st])
+    if st == DOMAIN_ERROR:
+        raise DomainError(STATUS_NAMES[st])
+
+
+def solve_kkt(solver: DenseSolver, prob: Problem, state: State, scaling: Scaling, dx, dy, dz, ds,
+              cx, cy, cz, cs):
+    """solve_kkt(::DenseSolver, ...) (densesolver.jl:54-90): writes (cx,cy,cz,cs)
+    in place and leaves (dx,dy,dz,ds) untouched."""
+    s, z = solver._sz if solver._sz is not None else (scaling.s, scaling.z)
+    out = batch_kkt_solve(prob.cones, prob.n, prob.m, prob.k, _colmajor(prob.A, prob.m, prob.n),
+                          _colmajor(prob.G, prob.k, prob.n), np.array([prob.sing], np.uint8), s, z,
+                          dx, dy, dz, ds, ctx=solver.ctx)
+    _raise_status(int(out["status"][0]))
+    cx[:] = out["cx"]
+    cy[:] = out["cy"]
+    cz[:] = out["cz"]
+    cs[:] = out["cs"]
+
+
+class SolverState:
+    """SolverState(prob, solver) (solver.jl:22-37): the scaling type comes from
+    the plugin (KKTSolver{S} -> S(pr)).  `maxit`, `tol` default to the reference
+    constants; after a solve `iters` and `status` hold the outcome."""
+
+    def __init__(self, prob: Problem, solver: DenseSolver, maxit=40, tol=1e-5):
+        self.scaling = solver.scaling_type(prob)
+        self.solver = solver
+        self.maxit, self.tol = maxit, tol
+        self.iters, self.status = 0, None
+
+
+def solve_socp(prob: Problem, ss: SolverState) -> State:
+    """solve_socp(prob, ss) (solver.jl:40-153) on the GPU.  Like the reference it
+    returns the final State, and raises where the reference throws."""
+    out = batch_solve(prob.cones, prob.n, prob.m, prob.k, prob.c, _colmajor(prob.A, prob.m, prob.n),
+                      prob.b, _colmajor(prob.G, prob.k, prob.n), prob.h,
+                      np.array([prob.sing], np.uint8), maxit=ss.maxit, tol=ss.tol,
+                      ctx=ss.solver.ctx)
+    ss.iters, ss.status = int(out["iters"][0]), int(out["status"][0])
+    _raise_status(ss.status)
+    return State(prob, out["x"], out["y"], out["z"], out["s"])
+
+
+def solve_socp_batched(problems, maxit=40, tol=1e-5, ctx=None):
+    """Batched solve of Problems sharing dims and cones; returns (states, iters, status)
+    without raising: failures are reported per problem."""
+    p0 = problems[0]
+    n, m, k = p0.n, p0.m, p0.k
+    for p in problems:
+        assert (p.n, p.m, p.k) == (n, m, k)
+    c = np.concatenate([p.c for p in problems])
+    A = np.concatenate([_colmajor(p.A, m, n) for p in problems]) if m else None
+    b = np.concatenate([p.b for p in problems]) if m else None
+    G = np.concatenate([_colmajor(p.G, k, n) for p in problems])
+    h = np.concatenate([p.h for p in problems])
+    sing = np.array([p.sing for p in problems], np.uint8)
+    out = batch_solve(p0.cones, n, m, k, c, A, b, G, h, sing, maxit=maxit, tol=tol, ctx=ctx)
+    states = [State(p, out["x"][i * n:(i + 1) * n], out["y"][i * m:(i + 1) * m],
+                    out["z"][i * k:(i + 1) * k], out["s"][i * k:(i + 1) * k])
+              for i, p in enumerate(problems)]
+    return states, out["iters"], out["status"]

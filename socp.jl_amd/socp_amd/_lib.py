@@ -1,0 +1,147 @@
+"""ctypes binding of libsocp.so (include/socp.h).
+
+The HIP library is the only compute path: if it is missing or no GPU is
+present, every solve raises.  There is no CPU fallback in the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # socp.jl_amd/
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libsocp.so")
+HEADER = os.path.join(os.path.dirname(_PKG_ROOT), "include", "socp.h")
+
+# return codes / statuses / flags (include/socp.h)
+SOCP_OK, SOCP_E_INVALID, SOCP_E_UNSUPPORTED, SOCP_E_HIP, SOCP_E_NOMEM = 0, -1, -2, -3, -4
+CONVERGED, MAXIT, CHOL_H_FAILED, CHOL_S_FAILED, DOMAIN_ERROR = 0, 1, 2, 3, 4
+CONE_POC, CONE_SOC = 0, 1
+F_DEVICE_PTRS, F_WARM_START = 1, 2
+
+EXPORTED = [
+    "socp_last_error", "socp_version", "socp_params_default", "socp_ctx_create",
+    "socp_ctx_destroy", "socp_ctx_sync", "socp_ctx_stream", "socp_supported",
+    "socp_batch_solve", "socp_batch_solve_ex", "socp_batch_kkt_solve", "socp_generate",
+    "socp_last_kernel_ms", "socp_last_kernel_name", "socp_debug_set_kkt_dump",
+]
+
+
+class SocpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libsocp error {code}: {msg}")
+        self.code = code
+
+
+class Dims(C.Structure):
+    _fields_ = [("batch", C.c_int64), ("n", C.c_int32), ("m", C.c_int32), ("k", C.c_int32),
+                ("ncones", C.c_int32)]
+
+
+class Params(C.Structure):
+    _fields_ = [("maxit", C.c_int32), ("sigma_exp", C.c_int32), ("tol", C.c_double),
+                ("step", C.c_double), ("init_eps", C.c_double), ("flags", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+def default_params(**kw) -> Params:
+    """socp_params with the reference constants (solver.jl:105,122,133,146,91)."""
+    p = Params(40, 3, 1e-5, 0.99, 1e-10, 0, 0)
+    for key, v in kw.items():
+        setattr(p, key, v)
+    return p
+
+
+_lib = None
+
+
+def load():
+    """Load libsocp.so; raises (loudly) if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libsocp.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    vp, i32p, dp, u8p = C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p
+    L.socp_last_error.restype = C.c_char_p
+    L.socp_version.restype = C.c_char_p
+    L.socp_params_default.argtypes = [C.POINTER(Params)]
+    L.socp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    L.socp_ctx_destroy.argtypes = [vp]
+    L.socp_ctx_sync.argtypes = [vp]
+    L.socp_ctx_stream.argtypes = [vp]
+    L.socp_ctx_stream.restype = C.c_void_p
+    L.socp_supported.argtypes = [C.POINTER(Dims)]
+    common = [vp, C.POINTER(Dims), i32p, i32p, i32p]
+    L.socp_batch_solve.argtypes = common + [dp] * 5 + [u8p, C.POINTER(Params)] + [dp] * 4 + [i32p, i32p]
+    L.socp_batch_solve_ex.argtypes = common + [dp] * 5 + [u8p, C.POINTER(Params)] + [dp] * 4 + [i32p, i32p, dp]
+    L.socp_batch_kkt_solve.argtypes = common + [dp, dp, u8p] + [dp] * 2 + [dp] * 4 + [dp] * 4 + [i32p, C.c_int32]
+    L.socp_generate.argtypes = common + [C.c_uint64, C.c_int64] + [dp] * 5
+    L.socp_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    L.socp_last_kernel_name.argtypes = [vp]
+    L.socp_last_kernel_name.restype = C.c_char_p
+    L.socp_debug_set_kkt_dump.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != 0:
+        raise SocpError(rc, load().socp_last_error().decode())
+
+
+def ptr(a) -> C.c_void_p:
+    """Raw pointer of a numpy array or a torch tensor (host or device); None passes NULL."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return C.c_void_p(a.ctypes.data)
+    return C.c_void_p(a.data_ptr())  # torch.Tensor
+
+
+class Context:
+    """One socp_ctx (a HIP stream on one device); one per host thread."""
+
+    def __init__(self, device: int = 0):
+        L = load()
+        h = C.c_void_p()
+        check(L.socp_ctx_create(device, C.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            load().socp_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(load().socp_ctx_sync(self.handle))
+
+    @property
+    def stream(self) -> int:
+        return load().socp_ctx_stream(self.handle)
+
+    def last_kernel_ms(self) -> float:
+        v = C.c_float()
+        check(load().socp_last_kernel_ms(self.handle, C.byref(v)))
+        return float(v.value)
+
+    def last_kernel_name(self) -> str:
+        return load().socp_last_kernel_name(self.handle).decode()
+
+
+_default_ctx = {}
+
+
+def default_context(device: int = 0) -> Context:
+    if device not in _default_ctx:
+        _default_ctx[device] = Context(device)
+    return _default_ctx[device]
