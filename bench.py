@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark: IPM problem-iterations/s on the BASELINE.json workload (config C2).
+
+A "step" is one batched solve of this rank's shard: 65,536 independent dense
+SOCPs (n=64, m=16, k=96, cones POC32+SOC32+SOC32) generated on the device,
+initial point + K=8 interior-point iterations each (fixed-K mode, tol=0,
+SURVEY.md §8(d)), plus (N>1) the all-gather of per-problem (status, iters)
+over RCCL — the path's only exchange step.  Shards are disjoint global
+problem ranges, so scaling is weak.
+
+Output: one JSON line on rank 0 (driver contract), including
+  roofline     — FP64 work of the solver kernel (SURVEY.md §8(d) formula,
+                 939.3 KFLOP per problem-iteration at C2) over its HIP-event
+                 duration on the solver's own stream, against the 78.6 TFLOP/s
+                 FP64 peak;
+  cpu_baseline — the CPU oracle (reference op order, oracle/) on a bounded
+                 sample of the same problems on this host's cores.
+Launch: python bench.py [--gpus N --steps K --warmup W]
+        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "socp.jl_amd"))
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 (vector = matrix), spec
+
+
+def flops_per_problem_iter(n, m, k, sing=False):
+    """SYRK + potrf/potri + A*Li + S + chol(S) + mat-vecs."""
+    return (n * (n + 1) * k + n ** 3 + 2 * m * n * n + m * (m + 1) * n + m ** 3 / 3.0
+            + 16 * k * n + 12 * m * n + 4 * n * n + 4 * m * m + (n * n if sing else 0))
+
+
+def bytes_per_problem_iter(n, m, k):
+    """G, A read once; c, b, h; x, y, z, s read + write."""
+    return 8 * (k * n + m * n) + 8 * (n + m + k) + 16 * (n + m + 2 * k)
+
+
+def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None):
+    """Oracle (the reference algorithm restated in C, oracle/) on host cores."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle as O  # test infrastructure: timed as the baseline, never the product
+    threads = threads or min(16, os.cpu_count() or 1)
+    chunk = 256
+    d = O.generate(cfg.cones, chunk, cfg.n, cfg.m, cfg.k, cfg.seed)
+    P = O.Params(maxit=fixed_k, tol=0.0)
+    sing = [0] * chunk
+    O.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"], sing=sing,
+                  params=P, nthreads=threads)  # warm-up
+    iters, t0, reps = 0, time.perf_counter(), 0
+    while True:
+        r = O.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                          sing=sing, params=P, nthreads=threads)
+        iters += int(r["iters"].sum())
+        reps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": iters / dt, "unit": "problem-iterations/s", "cores": threads, "kind": "port",
+            "sample": f"{reps}x{chunk} C2 problems (first {chunk} of the seeded workload), fixed-K={fixed_k}, "
+                      f"oracle/socp_oracle.c (reference op order incl. dense iW*iW' and potrs(I) inverse), "
+                      f"OpenMP {threads} threads, {dt:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--batch", type=int, default=0, help="problems per GPU (default: config batch)")
+    ap.add_argument("--fixed-k", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "r01_pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import socp_amd as S
+    from socp_amd.configs import CONFIGS
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cfg = CONFIGS["C2" if args.config == "C3" else args.config]
+    B = args.batch or cfg.batch
+    K = args.fixed_k or cfg.fixed_k
+    n, m, k = cfg.n, cfg.m, cfg.k
+    ctx = S.Context(local)
+    c, A, b, G, h = S.generate(cfg.cones, B, n, m, k, cfg.seed, first_problem=rank * B, ctx=ctx)
+    sing = torch.zeros(B, dtype=torch.uint8, device=dev)  # G (96x64 uniform) has full column rank
+    ctx.sync()
+    out = None
+    gathered = torch.empty((world, B, 2), dtype=torch.int32, device=dev) if world > 1 else None
+
+    def step():
+        nonlocal out
+        out = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=0.0, ctx=ctx, out=out)
+        if world > 1:
+            ctx.sync()
+            local_st = torch.stack([out["status"], out["iters"]], dim=1)
+            dist.all_gather_into_tensor(gathered.view(-1, 2), local_st)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kernel_ms.append(ctx.last_kernel_ms())  # HIP events around the solver launch
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    iters_local = int(out["iters"].sum().item()) * args.steps
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        it = torch.tensor([iters_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(it)
+        iters_total = int(it.item())
+    else:
+        iters_total = iters_local
+    status_counts = torch.bincount(out["status"].long(), minlength=5).tolist()
+
+    if rank == 0:
+        kms = sum(kernel_ms) / len(kernel_ms)
+        iters_per_launch = int(out["iters"].sum().item())
+        F = flops_per_problem_iter(n, m, k)
+        achieved = F * iters_per_launch / (kms * 1e-3) / 1e12
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("config") == cfg.name and tj.get("batch") == B and tj.get("fixed_k") == K:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "IPM iters/sec, 65k-batch n=64 dense SOCP at 1/2/4/8 GPU; achieved HBM GB/s",
+            "value": iters_total / dt,
+            "unit": "problem-iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (device SplitMix64 generator, SURVEY.md §8(d); feasible by construction)",
+            "config": {
+                "workload": f"{cfg.name}: {B} problems per GPU, n={n}, m={m}, k={k}, cones POC32+SOC32+SOC32, "
+                            f"initial point + fixed-K={K} IPM iterations (tol=0)",
+                "global_batch": B * world,
+                "parallelism": f"dp{world} (disjoint problem shards, status all-gather only)",
+            },
+            "kernel": ctx.last_kernel_name(),
+            "kernel_ms": kms,
+            "status_counts": status_counts,
+            "roofline": {
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP64_PEAK_TFLOPS,
+                "traffic": traffic,
+                "flops_per_problem_iter": F,
+                "problem_iters_per_launch": iters_per_launch,
+            },
+        }
+        if not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,86 @@
+"""The C-ABI library (libsocp.so) and the host-side mirror, without a GPU."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import socp_amd as S
+from socp_amd import _lib
+from socp_amd.configs import CONFIGS
+from problems import kat_problem
+
+
+def _header_functions():
+    txt = open(_lib.HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(socp_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_built_and_loads():
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build() first"
+    L = _lib.load()
+    assert L.socp_version().decode().startswith("socp-mi355x")
+
+
+def test_exports_every_declared_symbol():
+    L = C.CDLL(_lib.LIB_PATH)
+    declared = _header_functions()
+    assert len(declared) >= 14
+    missing = [f for f in declared if not hasattr(L, f)]
+    assert not missing, missing
+    assert set(_lib.EXPORTED) == set(declared)
+
+
+def test_default_params_are_reference_constants():
+    p = _lib.Params()
+    _lib.load().socp_params_default(C.byref(p))
+    # solver.jl:105 (maxit 40), :122 (tol 1e-5), :133 (sigma^3), :146 (0.99), :91,97 (1e-10)
+    assert (p.maxit, p.sigma_exp, p.tol, p.step, p.init_eps, p.flags) == (40, 3, 1e-5, 0.99, 1e-10, 0)
+
+
+def test_supported_dims():
+    L = _lib.load()
+    for name, ok in (("C0b", True), ("C1", True), ("C2", True), ("C4", False)):
+        cfg = CONFIGS[name]
+        d = _lib.Dims(cfg.batch, cfg.n, cfg.m, cfg.k, len(cfg.cones))
+        assert bool(L.socp_supported(C.byref(d))) == ok, name
+
+
+def test_null_context_is_an_api_error():
+    L = _lib.load()
+    d = _lib.Dims(1, 3, 0, 4, 2)
+    rc = L.socp_batch_solve(None, C.byref(d), None, None, None, None, None, None, None, None, None, None,
+                            None, None, None, None, None, None)
+    assert rc == _lib.SOCP_E_INVALID
+    assert b"ctx" in L.socp_last_error()
+
+
+def test_problem_mirror_asserts_and_sing(kats):
+    # Problem(c, A, b, G, h, cones): shape asserts (Socp.jl:43-47) and `sing` (Socp.jl:49-56)
+    cones, c, A, b, G, h = kat_problem(kats["soc3"])
+    p = S.Problem(c, A, b, G, h, cones)
+    assert (p.n, p.m, p.k, p.sing) == (3, 1, 7, False)
+    with pytest.raises(AssertionError):
+        S.Problem(c, A, b[:0], G, h, cones)
+    with pytest.raises(AssertionError):
+        S.Problem(c, A, b, G, h[:-1], cones)
+    sing_prob = S.Problem(np.zeros(10), np.ones((8, 10)), np.ones(8), np.ones((3, 10)), np.ones(3), [S.SOC(0, 3)])
+    assert sing_prob.sing
+    with pytest.raises(AssertionError):
+        S.State(p, np.zeros(2), np.zeros(1), np.zeros(7), np.zeros(7))
+
+
+def test_cone_arrays():
+    kind, offs, dim = S.cone_arrays([S.POC(0, 32), S.SOC(32, 32), (1, 64, 32)])
+    assert kind.tolist() == [0, 1, 1] and offs.tolist() == [0, 32, 64] and dim.tolist() == [32, 32, 32]
+
+
+def test_flop_and_byte_model():
+    import bench
+    # C1 134.3 K, C2 939.3 K, C4 344.8 M flop; C2 63.1 KB
+    assert abs(bench.flops_per_problem_iter(32, 8, 48) - 134.3e3) < 0.1e3
+    assert abs(bench.flops_per_problem_iter(64, 16, 96) - 939.3e3) < 0.1e3
+    assert abs(bench.flops_per_problem_iter(512, 64, 640) - 344.8e6) < 0.1e6
+    assert abs(bench.bytes_per_problem_iter(64, 16, 96) - 63.1e3) < 0.1e3

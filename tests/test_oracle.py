@@ -1,0 +1,164 @@
+"""The CPU oracle against every known-answer vector of the reference's
+test/runtests.jl (transcribed in tests/golden/reference_kats.json).  CPU only."""
+import numpy as np
+import pytest
+
+from problems import kat_problem, optimal_control
+
+
+def test_vector_ops_exact(kats, oracle):
+    # runtests.jl:10-28 — these are `==` tests in the reference
+    v = kats["vector_ops"]
+    cones = [tuple(c) for c in v["cones"]]
+    t1, t2 = np.array(v["tv1"], float), np.array(v["tv2"], float)
+    assert np.array_equal(oracle.vprod(cones, t1, t1), v["vprod_tv1_tv1"])
+    assert np.array_equal(oracle.vprod(cones, t1, t2), v["vprod_tv1_tv2"])
+    assert np.linalg.norm(oracle.vprod(cones, t1, oracle.iprod(cones, t1, t2)) - t2) < 1e-12
+    e = oracle.make_e(cones, 6)
+    assert np.array_equal(oracle.vprod(cones, e, t1), t1)
+    assert np.array_equal(oracle.vprod(cones, e, t2), t2)
+    for case in v["cgt_cases"]:
+        cc = [tuple(c) for c in case["cones"]]
+        assert oracle.cgt(cc, np.array(case["x"], float), np.array(case["dx"], float)) == case["expect"]
+    ms = v["max_step_cases"]
+    assert oracle.max_step([tuple(c) for c in ms[0]["cones"]], np.array(ms[0]["x"], float)) == -1.0
+    assert oracle.max_step([tuple(c) for c in ms[1]["cones"]], np.array(ms[1]["x"], float)) == np.sqrt(2 ** 2 + 3 ** 2) - 1.0
+    assert oracle.max_step([tuple(c) for c in ms[2]["cones"]], np.array(ms[2]["x"], float)) == np.sqrt(2 ** 2 + 3 ** 2) - 1.0
+
+
+def test_deg(oracle):
+    assert oracle.deg([(0, 0, 3), (1, 3, 3)]) == 4  # vectors.jl:165-179
+
+
+def test_nt_scaling_identities(kats, oracle):
+    # runtests.jl:30-48, tightened from 1e-3 to 1e-12
+    q = kats["nt_scaling"]
+    cones = [tuple(c) for c in q["cones"]]
+    s, z = np.array(q["s"], float), np.array(q["z"], float)
+    sc = oracle.compute_scaling(cones, s, z)
+    W, iW, l = sc["W"], sc["iW"], sc["l"]
+    assert sc["status"] == 0
+    assert np.abs(iW @ W - np.eye(6)).max() < 1e-12
+    assert np.linalg.norm(iW.T @ s - W @ z) < 1e-12
+    assert np.linalg.norm(iW.T @ s - l) < 1e-12
+    op = oracle.scale(cones, sc["wbs"], sc["mu"], z)
+    assert np.linalg.norm(W @ z - op) < 1e-12
+    op2 = oracle.scale(cones, sc["wbs"], sc["mu"], op, inverse=True)
+    assert np.linalg.norm(z - op2) < 1e-12
+    assert np.abs(sc["iWiW"] - iW @ iW.T).max() < 1e-12
+
+
+def _sqr_scaling_iWiW(cones, s, z):
+    """Independent restatement of the SqrScaling W^-2 = D + uu' - vv' algebra
+    (sqrscalings.jl:66-139, compute_full_scaling :196-214) used to cross-check the
+    oracle's dense iWiW (runtests.jl:79-89)."""
+    k = len(s)
+    out = np.zeros((k, k))
+    for kind, o, d in cones:
+        if kind == 0:
+            for i in range(o, o + d):
+                out[i, i] = z[i] / s[i]
+            continue
+        sb, zb = s[o:o + d].copy(), z[o:o + d].copy()
+        sp = sb[0] ** 2 - sb[1:] @ sb[1:]
+        zp = zb[0] ** 2 - zb[1:] @ zb[1:]
+        sb /= np.sqrt(sp)
+        zb /= np.sqrt(zp)
+        gamma = np.sqrt((1 + zb @ sb) / 2)
+        wb = np.concatenate([[sb[0] + zb[0]], sb[1:] - zb[1:]]) / (2 * gamma)
+        inusq = 1 / np.sqrt(sp / zp)
+        inu = 1 / np.sqrt(np.sqrt(sp / zp))
+        wb0, wb1 = wb[0], wb[1:]
+        wb1sq = wb1 @ wb1
+        cv = -(1 + wb0 + wb1sq / (1 + wb0))
+        dd = 1 + 2 / (1 + wb0) + wb1sq / (1 + wb0) ** 2
+        a = (wb0 * wb0 + wb1sq - cv * cv * wb1sq / (1 + dd * wb1sq)) / 2
+        u0 = np.sqrt(wb0 * wb0 + wb1sq - a)
+        u1 = cv / u0
+        v1 = np.sqrt(cv * cv / (u0 * u0) - dd)
+        D = np.full(d, inusq)
+        D[0] = a * inusq
+        u = inu * np.concatenate([[u0], u1 * wb1])
+        v = inu * np.concatenate([[0.0], v1 * wb1])
+        out[o:o + d, o:o + d] = np.diag(D) + np.outer(u, u) - np.outer(v, v)
+    return out
+
+
+def test_sqr_scaling_identity(kats, oracle):
+    # runtests.jl:79-89: compute_full_scaling(SqrScaling) == Scaling.iWiW on two (u,v) pairs
+    q = kats["sqr_scaling"]
+    cones = [tuple(c) for c in q["cones"]]
+    for pair in q["pairs"]:
+        s, z = np.array(pair["s"]), np.array(pair["z"])
+        sc = oracle.compute_scaling(cones, s, z)
+        assert np.abs(_sqr_scaling_iWiW(cones, s, z) - sc["iWiW"]).max() < 1e-10
+
+
+def test_kkt_golden(kats, oracle):
+    # runtests.jl:95-128; the reference asserts 1e-3, the gate here is P2 (1e-10)
+    g = kats["kkt_golden"]
+    cones = [tuple(c) for c in g["cones"]]
+    r = oracle.kkt_single(cones, np.zeros((0, 3)), np.array(g["G"]), False, np.array(g["s"]), np.array(g["z"]),
+                          np.array(g["dx"]), np.zeros(0), np.array(g["dz"]), np.array(g["ds"]))
+    assert r["status"] == 0
+    for key in ("cx", "cz", "cs"):
+        assert np.abs(r[key] - np.array(g[key])).max() < 1e-10, key
+
+
+@pytest.mark.parametrize("name", ["soc1", "soc2", "soc3"])
+def test_end_to_end_kats(kats, oracle, name):
+    # runtests.jl:130-191
+    q = kats[name]
+    cones, c, A, b, G, h = kat_problem(q)
+    r = oracle.solve_trace(cones, c, A, b, G, h)
+    assert r["status"] == 0
+    assert np.linalg.norm(r["x"] - np.array(q["x_expect"])) < q["tol"]
+
+
+def test_optimal_control_converges(oracle):
+    # runtests.jl:204-244 (the reference only prints); sing problem: G is 50 x 150
+    cones, c, A, b, G, h = optimal_control(50)
+    assert oracle.sing_flag(G)
+    r = oracle.solve_trace(cones, c, A, b, G, h)
+    assert r["status"] == 0 and r["iters"] <= 40
+    assert np.linalg.norm(A @ r["x"] - b) < 1e-6
+    # the bound on the applied force is tight at the optimum: t >= |force|
+    force = r["x"][100:149]
+    assert r["x"][-1] >= np.linalg.norm(force) - 1e-4
+
+
+def test_init_lu_matches_kkt_route(oracle):
+    """The initial point (solver.jl:68-104) by dense LU equals the KKT system with
+    W = I, lam = e, ds = 0 (the route the GPU takes)."""
+    from socp_amd.configs import C1, C2
+    for cfg in (C1, C2):
+        d = oracle.generate(cfg.cones, 3, cfg.n, cfg.m, cfg.k, cfg.seed)
+        for p in range(3):
+            from problems import batch_problem
+            c, A, b, G, h = batch_problem(d, 3, cfg.n, cfg.m, cfg.k, p)
+            ip = oracle.init_point(cfg.cones, c, A, b, G, h, params=oracle.Params(init_eps=-1.0))
+            e = oracle.make_e(cfg.cones, cfg.k)
+            r = oracle.kkt_single(cfg.cones, A, G, False, e, e, -c, b, h, np.zeros(cfg.k))
+            assert np.abs(r["cx"] - ip["x"]).max() < 1e-10 * max(1, np.abs(ip["x"]).max())
+            assert np.abs(r["cy"] - ip["y"]).max() < 1e-10 * max(1, np.abs(ip["y"]).max())
+
+
+def test_generator_deterministic_and_shardable(oracle):
+    from socp_amd.configs import C1
+    cfg = C1
+    a = oracle.generate(cfg.cones, 6, cfg.n, cfg.m, cfg.k, cfg.seed, first_problem=0)
+    b = oracle.generate(cfg.cones, 2, cfg.n, cfg.m, cfg.k, cfg.seed, first_problem=4)
+    for key, L in (("c", cfg.n), ("A", cfg.m * cfg.n), ("b", cfg.m), ("G", cfg.k * cfg.n), ("h", cfg.k)):
+        assert np.array_equal(a[key][4 * L:6 * L], b[key]), key
+    # feasible by construction: G x0 + s0 = h with s0 interior -> strict cone membership of s0
+    # is exercised through the solver; here check the data is finite and nontrivial
+    assert np.isfinite(a["G"]).all() and np.abs(a["G"]).max() <= 1.0
+
+
+def test_fixed_k_mode(oracle):
+    from socp_amd.configs import C2
+    cfg = C2
+    d = oracle.generate(cfg.cones, 4, cfg.n, cfg.m, cfg.k, cfg.seed)
+    r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                           params=oracle.Params(maxit=3, tol=0.0))
+    assert (r["status"] == 1).all() and (r["iters"] == 3).all()
