@@ -164,6 +164,12 @@ const char* socp_last_kernel_name(socp_ctx* ctx);
  * lambda and wbar (scalings.jl:1-20).  NULL disables. */
 int socp_debug_set_kkt_dump(double* dev_buf);
 
+/* Diagnostic hook: device buffer of 13 uint64 counters; in the phase-stamp build
+ * (libsocp_stamps.so, -DSOCP_STAMPS) every solve adds per-phase shader-clock
+ * cycles (load, scaling, residuals, U, SYRK, sweep(H), Schur, solve, step, init,
+ * store, other) and the executed iterations.  The product build ignores it. */
+int socp_debug_set_stamps(unsigned long long* dev_buf);
+
 #ifdef __cplusplus
 }
 #endif

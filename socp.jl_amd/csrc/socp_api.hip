@@ -62,7 +62,11 @@ struct socp_ctx {
 };
 
 extern "C" const char* socp_last_error(void) { return g_err.c_str(); }
+#ifdef SOCP_STAMPS
+extern "C" const char* socp_version(void) { return "socp-mi355x 0.1 (gfx950, phase-stamp diagnostic build)"; }
+#else
 extern "C" const char* socp_version(void) { return "socp-mi355x 0.1 (gfx950)"; }
+#endif
 
 extern "C" void socp_params_default(socp_params* p) {
   p->maxit = 40;
@@ -174,6 +178,8 @@ extern "C" int socp_supported(const socp_dims* d) {
 }
 
 // ---------------------------------------------------------------- launch
+static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_STAMPS builds)
+
 static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
   size_t lds = small_lds_bytes(v->NQ, v->NP, v->MQ);
   if (lds > 160 * 1024) return fail(SOCP_E_UNSUPPORTED, "LDS footprint too large");
@@ -186,6 +192,7 @@ static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
   if (blocks > args.B) blocks = args.B;
   if (blocks < 1) blocks = 1;
   HIPCHK(hipMemsetAsync(args.counter, 0, sizeof(int32_t), ctx->stream));
+  args.stamps = g_stamps;
   void* kargs[] = {&args};
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
   HIPCHK(hipLaunchKernel(v->kernel, dim3((unsigned)blocks), dim3(64), kargs, lds, ctx->stream));
@@ -319,6 +326,10 @@ extern "C" int socp_batch_solve(socp_ctx* ctx, const socp_dims* dims, const int3
 }
 
 static double* g_kkt_debug = nullptr;  // device buffer for socp_debug_kkt (testing hook)
+extern "C" int socp_debug_set_stamps(unsigned long long* dev_buf) {
+  g_stamps = dev_buf;
+  return 0;
+}
 
 extern "C" int socp_debug_set_kkt_dump(double* dev_buf) {
   g_kkt_debug = dev_buf;
@@ -403,6 +414,18 @@ struct GenArgs {
   ConeTable cones;
 };
 
+// The generator must round exactly like the oracle (gcc -ffp-contract=off):
+// hipcc contracts a*b+c into v_fma_f64 by default, and __dadd_rn/__dmul_rn are
+// plain operators, so contraction is switched off for these functions (the
+// build uses -ffp-contract=fast-honor-pragmas so the pragma is obeyed).
+#pragma clang fp contract(off)
+// local operators: the bodies of HIP's __dadd_rn/__dmul_rn lie outside this
+// pragma and would still be fused
+__device__ __forceinline__ double add_rn(double x, double y) { return x + y; }
+__device__ __forceinline__ double sub_rn(double x, double y) { return x - y; }
+__device__ __forceinline__ double mul_rn(double x, double y) { return x * y; }
+__device__ __forceinline__ double sqrt_rn(double x) { return __builtin_sqrt(x); }
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -411,10 +434,10 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 }
 __device__ __forceinline__ double gen_u(uint64_t seed, uint64_t p, uint64_t e) {
   uint64_t u = splitmix64(seed ^ ((p << 24) | e));
-  return __dmul_rn((double)(u >> 11), 0x1.0p-53);
+  return mul_rn((double)(u >> 11), 0x1.0p-53);
 }
 __device__ __forceinline__ double gen_sym(uint64_t seed, uint64_t p, uint64_t e) {
-  return __dsub_rn(__dmul_rn(2.0, gen_u(seed, p, e)), 1.0);
+  return sub_rn(mul_rn(2.0, gen_u(seed, p, e)), 1.0);
 }
 
 __global__ void __launch_bounds__(256) socp_generate_kernel(GenArgs a) {
@@ -441,8 +464,8 @@ __global__ void __launch_bounds__(256) socp_generate_kernel(GenArgs a) {
     const int o = a.cones.offs[c], d = a.cones.dim[c];
     const uint64_t es = base2 + 2 * (uint64_t)o, ez = es + d;
     if (a.cones.kind[c] == POC_K) {
-      s0[i] = __dadd_rn(0.5, gen_u(a.seed, gp, es + (i - o)));
-      z0[i] = __dadd_rn(0.5, gen_u(a.seed, gp, ez + (i - o)));
+      s0[i] = add_rn(0.5, gen_u(a.seed, gp, es + (i - o)));
+      z0[i] = add_rn(0.5, gen_u(a.seed, gp, ez + (i - o)));
     } else if (i > o) {
       s0[i] = gen_sym(a.seed, gp, es + (i - o - 1));
       z0[i] = gen_sym(a.seed, gp, ez + (i - o - 1));
@@ -455,34 +478,35 @@ __global__ void __launch_bounds__(256) socp_generate_kernel(GenArgs a) {
     const uint64_t es = base2 + 2 * (uint64_t)o, ez = es + d;
     double qs = 0.0, qz = 0.0;
     for (int i = 1; i < d; ++i) {
-      qs = __dadd_rn(qs, __dmul_rn(s0[o + i], s0[o + i]));
-      qz = __dadd_rn(qz, __dmul_rn(z0[o + i], z0[o + i]));
+      qs = add_rn(qs, mul_rn(s0[o + i], s0[o + i]));
+      qz = add_rn(qz, mul_rn(z0[o + i], z0[o + i]));
     }
-    s0[o] = __dadd_rn(__dadd_rn(__dsqrt_rn(qs), 0.5), gen_u(a.seed, gp, es + d - 1));
-    z0[o] = __dadd_rn(__dadd_rn(__dsqrt_rn(qz), 0.5), gen_u(a.seed, gp, ez + d - 1));
+    s0[o] = add_rn(add_rn(sqrt_rn(qs), 0.5), gen_u(a.seed, gp, es + d - 1));
+    z0[o] = add_rn(add_rn(sqrt_rn(qz), 0.5), gen_u(a.seed, gp, ez + d - 1));
   }
   __syncthreads();
   for (int i = threadIdx.x; i < k; i += blockDim.x) {
     double acc = 0.0;
     for (int j = 0; j < n; ++j)
-      acc = __dadd_rn(acc, __dmul_rn(gen_sym(a.seed, gp, (uint64_t)j * k + i), x0[j]));
-    a.h[p * k + i] = __dadd_rn(acc, s0[i]);
+      acc = add_rn(acc, mul_rn(gen_sym(a.seed, gp, (uint64_t)j * k + i), x0[j]));
+    a.h[p * k + i] = add_rn(acc, s0[i]);
   }
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
     double acc = 0.0;
     for (int j = 0; j < n; ++j)
-      acc = __dadd_rn(acc, __dmul_rn(gen_sym(a.seed, gp, kn + (uint64_t)j * m + i), x0[j]));
+      acc = add_rn(acc, mul_rn(gen_sym(a.seed, gp, kn + (uint64_t)j * m + i), x0[j]));
     a.b[p * m + i] = acc;
   }
   for (int j = threadIdx.x; j < n; j += blockDim.x) {
     double t = 0.0, u = 0.0;
     for (int i = 0; i < m; ++i)
-      t = __dadd_rn(t, __dmul_rn(gen_sym(a.seed, gp, kn + (uint64_t)j * m + i), y0[i]));
+      t = add_rn(t, mul_rn(gen_sym(a.seed, gp, kn + (uint64_t)j * m + i), y0[i]));
     for (int i = 0; i < k; ++i)
-      u = __dadd_rn(u, __dmul_rn(gen_sym(a.seed, gp, (uint64_t)j * k + i), z0[i]));
-    a.c[p * n + j] = -__dadd_rn(t, u);
+      u = add_rn(u, mul_rn(gen_sym(a.seed, gp, (uint64_t)j * k + i), z0[i]));
+    a.c[p * n + j] = -add_rn(t, u);
   }
 }
+#pragma clang fp contract(on)
 }  // namespace
 
 extern "C" int socp_generate(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,

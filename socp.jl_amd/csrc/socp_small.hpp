@@ -3,11 +3,11 @@
 // One 64-lane wavefront owns one problem for its whole solve (persistent
 // one-wave blocks pull problem indices from an atomic work counter).  The
 // problem's G (k x n, the dominant data: 48 KiB at n=64,k=96) is loaded from
-// HBM once per solve and stays in registers for every iteration, laid out as
-// the B-operand fragment of v_mfma_f64_16x16x4_f64:
+// HBM once per solve and stays in AGPRs for every iteration, laid out as the
+// B-operand fragment of v_mfma_f64_16x16x4_f64:
 //     lane (g = lane>>4, cl = lane&15) holds G[4p+g][16q+cl] in G[p][q].
 // Per iteration (reference solver.jl:105-151):
-//   - NT scaling (scalings.jl:22-110) with per-cone segmented wave reductions;
+//   - NT scaling (scalings.jl:22-110) with per-cone segmented DPP scans;
 //   - residuals (solver.jl:110-122) from register G;
 //   - H = X'X with X = W^-1 G generated in registers and contracted by f64
 //     MFMA: the reference's iWiW GEMM, G'*iWiW and *G (scalings.jl:108,
@@ -20,9 +20,10 @@
 // LDS (<40 KiB per wave at n=64) holds only vectors, A and broadcast scratch,
 // so four one-wave blocks (one per SIMD) share a CU.
 //
-// Code-size discipline: the solve, the factorisation and every cone vector
-// op have exactly one instance in the kernel (phase machine + the shared
-// out-of-line cone_vop), which keeps the instruction stream cache-resident.
+// Code-size discipline: the driver is a micro-phase loop in which the cone
+// vector op, the factorisation, the KKT solve body and the residuals each
+// have exactly one inlined instance (no calls: a call would force the live
+// H/Li tiles out of registers), keeping the instruction stream cache-resident.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -61,12 +62,13 @@ struct SmallArgs {
   const double *dx, *dy, *dz, *ds;
   double *cx, *cy, *cz, *cs;
   int32_t* counter;
-  double* dbg;  // optional (KKT mode): per problem H[n*n], Li[n*n], lam[k], wb[k]
+  double* dbg;                 // optional (KKT mode): per problem H[n*n], Li[n*n], lam[k], wb[k]
+  unsigned long long* stamps;  // SOCP_STAMPS builds: per-phase cycle totals
   ConeTable cones;
 };
 
 // ------------------------------------------------------------ LDS layout
-// Fixed region (independent of the template shape, used by cone_vop):
+// Fixed region (independent of the template shape):
 enum : int {
   O_RC = 0,                  // rcode[KMAX]: cone*4 + type (0 POC, 1 SOC head, 2 SOC tail, 3 pad)
   O_COFF = O_RC + KMAX,      // cone offs[NCS]
@@ -76,7 +78,8 @@ enum : int {
   O_I1 = O_MU + NCS,         // 1/(1+wb0) per cone
   O_TOT = O_I1 + NCS,        // reduced values per cone [NCS][4]
   O_PART = O_TOT + 4 * NCS,  // per-slot partials [2][NCS][4]
-  O_KV = O_PART + 8 * NCS,   // 16 k-vectors of KMAX
+  O_CST = O_PART + 8 * NCS,  // step-length scratch per cone [NCS][4]
+  O_KV = O_CST + 4 * NCS,    // 16 k-vectors of KMAX
   O_FIXED_END = O_KV + 16 * KMAX
 };
 // k-vector ids
@@ -107,6 +110,21 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
   return (size_t)total * sizeof(double);
 }
 
+// Diagnostic phase timing (separate build, -DSOCP_STAMPS): per-phase s_memtime
+// deltas accumulated per problem and added to a global table by lane 0.
+#ifdef SOCP_STAMPS
+#define NSTAMP 12
+#define STAMP_DECL uint64_t st_last = 0; uint64_t st_acc[NSTAMP] = {0};
+#define STAMP_START_S(obj) do { __builtin_amdgcn_s_waitcnt(0); (obj).st_last = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP(i) do { __builtin_amdgcn_s_waitcnt(0); const uint64_t t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_last; st_last = t_; } while (0)
+#else
+#define STAMP_DECL
+#define STAMP_START_S(obj) do {} while (0)
+#define STAMP(i) do {} while (0)
+#endif
+enum { SP_LOAD, SP_SCALING, SP_RESID, SP_U, SP_SYRK, SP_SWEEP_H, SP_SCHUR, SP_SOLVE, SP_STEP, SP_VOP,
+       SP_STORE, SP_OTHER };
+
 extern __shared__ double socp_lds[];
 #define LDS(i) socp_lds[(i)]
 #define SYNC() __syncthreads()
@@ -128,20 +146,21 @@ __device__ __forceinline__ double a_get(const AD& r) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// a_get for a value consumed directly as an MFMA A/B operand: v_accvgpr_read is
+// a VALU write, and VALU write -> MFMA operand read needs 2 wait states, which
+// hipcc does not insert for a producer inside inline asm (it pads one state).
+__device__ __forceinline__ double a_get_mfma(const AD& r) {
+  uint32_t lo, hi;
+  asm("v_accvgpr_read_b32 %0, %2\n\tv_accvgpr_read_b32 %1, %3\n\ts_nop 1"
+      : "=v"(lo), "=v"(hi)
+      : "a"(r.lo), "a"(r.hi));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ double wmax(double v) {
-#pragma unroll
-  for (int o = 32; o; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-  return v;
-}
 __device__ __forceinline__ double sel4(d4 t, int r) {
   double v = t[0];
   v = (r == 1) ? t[1] : v;
@@ -150,315 +169,75 @@ __device__ __forceinline__ double sel4(d4 t, int r) {
   return v;
 }
 
-// --------------------------------------------------------- cone vector ops
-enum : int { VOP_SCALE, VOP_ISCALE, VOP_PAIR, VOP_IPROD, VOP_VPROD, VOP_SCALING, VOP_STEP,
-             VOP_MAXSTEP };
-
-struct VopResult {
-  double r0, r1;
-  int dom;
-};
-
-// Per-cone segmented reduction of up to 3 values over the compact layout
-// (element i = 64*slot + lane): inclusive Kogge-Stone scan inside each
-// cone's lane range, partials per slot in LDS, totals in LDS[O_TOT + c*4+v].
-// SOC segments are summed; POC segments take the max when poc_max is set.
-__device__ __forceinline__ void seg_reduce3(double (&vals)[2][3], int nv, bool poc_max, int k,
-                                            int nc, const int (&ci)[2], const int (&ssl)[2],
-                                            const int (&sle)[2], const bool (&ismax)[2]) {
-  const int lane = threadIdx.x;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    if (64 * s < k) {
-      double x[3] = {vals[s][0], vals[s][1], vals[s][2]};
-      const bool mx = poc_max && ismax[s];
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const bool ok = (lane - off) >= ssl[s];
-#pragma unroll
-        for (int v = 0; v < 3; ++v) {
-          if (v < nv) {
-            double y = __shfl_up(x[v], off);
-            double r = mx ? fmax(x[v], y) : x[v] + y;
-            x[v] = ok ? r : x[v];
-          }
-        }
-      }
-      if (lane == sle[s]) {
-#pragma unroll
-        for (int v = 0; v < 3; ++v) LDS(O_PART + (s * NCS + ci[s]) * 4 + v) = x[v];
-      }
-    }
-  }
-  SYNC();
-  if (lane < nc) {
-    const int c = lane;
-    const int o = (int)LDS(O_COFF + c), d = (int)LDS(O_CDIM + c);
-    const bool mx = poc_max && (int)LDS(O_CKIND + c) == POC_K;
-    const int s0 = o >> 6, s1 = (o + d - 1) >> 6;
-#pragma unroll
-    for (int v = 0; v < 3; ++v) {
-      double t = LDS(O_PART + (s0 * NCS + c) * 4 + v);
-      if (s1 > s0) {
-        double u = LDS(O_PART + (s1 * NCS + c) * 4 + v);
-        t = mx ? fmax(t, u) : t + u;
-      }
-      LDS(O_TOT + c * 4 + v) = t;
-    }
-  }
-  SYNC();
+// DPP move of a double (two 32-bit halves).  CTRL: 0x111+s = row_shr:s+1,
+// 0x142 = row_bcast:15, 0x143 = row_bcast:31 (GFX9 DPP); RM = row mask.
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int l2 = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, 0xF, false);
+  const int h2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, 0xF, false);
+  return __hiloint2double(h2, l2);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
 }
 
-// One out-of-line instance for every per-cone vector operation.  a, b, o1, o2
-// are LDS offsets of k-vectors.  Reference: scale!/iscale! (scalings.jl:112-173),
-// iprod!/vprod! (vectors.jl:58-125), compute_scaling (scalings.jl:22-99),
-// compute_step/scmax (mats.jl:30-86), max_step (mats.jl:1-28).
-static __device__ __noinline__ VopResult cone_vop(int op, int a, int b, int o1, int o2, int k, int nc) {
-  const int lane = threadIdx.x;
-  int ci[2], kd[2], eo[2], ssl[2], sle[2];
-  bool ev[2], hd[2], tail[2], poc[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int i = 64 * s + lane;
-    ev[s] = i < k;
-    const int code = ev[s] ? (int)LDS(O_RC + i) : 3;
-    const int c = ev[s] ? (code >> 2) : 0;
-    ci[s] = c;
-    kd[s] = ev[s] ? (code & 3) : 3;
-    hd[s] = kd[s] == 1;
-    tail[s] = kd[s] == 2;
-    poc[s] = kd[s] == 0;
-    const int o = ev[s] ? (int)LDS(O_COFF + c) : i;
-    const int d = ev[s] ? (int)LDS(O_CDIM + c) : 1;
-    eo[s] = o;
-    const int st = o > 64 * s ? o : 64 * s;
-    const int en = (o + d) < 64 * (s + 1) ? (o + d) : 64 * (s + 1);
-    ssl[s] = ev[s] ? st - 64 * s : lane;
-    sle[s] = ev[s] ? en - 1 - 64 * s : -1;
+// Inclusive segmented scan over the 64 lanes with DPP (row_shr 1,2,4,8 then
+// row_bcast 15/31): lane l accumulates lanes [max(ssl, 0) .. l] with op
+// (sum, or max when mx).  ssl = first lane of l's segment.
+template <int V>
+__device__ __forceinline__ void dpp_scan(double (&x)[V], int lane, int ssl, bool mx) {
+  const int rl = lane & 15;
+#define SOCP_SCAN_STEP(CTRL, RM, OK)                                 \
+  {                                                                  \
+    const bool ok_ = (OK);                                           \
+    _Pragma("unroll") for (int v = 0; v < V; ++v) {                  \
+      const double y = dpp<CTRL, RM>(x[v]);                          \
+      const double r = mx ? fmax(x[v], y) : x[v] + y;                \
+      x[v] = ok_ ? r : x[v];                                         \
+    }                                                                \
   }
-  const int LAM = kv(KV_LAM), WB = kv(KV_WB);
-  double v[2][3];
-  int nv = 1;
-  bool pmax = false;
-  VopResult R = {0.0, 0.0, 0};
-  // ---------------- phase 1: reduction inputs
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int i = 64 * s + lane;
-    v[s][0] = v[s][1] = v[s][2] = 0.0;
-    if (op == VOP_SCALE || op == VOP_ISCALE) {
-      v[s][0] = tail[s] ? LDS(WB + i) * LDS(a + i) : 0.0;
-    } else if (op == VOP_PAIR) {
-      v[s][0] = tail[s] ? LDS(WB + i) * LDS(a + i) : 0.0;
-      v[s][1] = tail[s] ? LDS(WB + i) * LDS(b + i) : 0.0;
-    } else if (op == VOP_IPROD) {
-      const double li = LDS(LAM + i);
-      v[s][0] = tail[s] ? li * li : 0.0;
-      v[s][1] = tail[s] ? LDS(a + i) * li : 0.0;
-    } else if (op == VOP_VPROD) {
-      v[s][0] = (tail[s] || hd[s]) ? LDS(a + i) * LDS(b + i) : 0.0;
-    } else if (op == VOP_SCALING) {  // a = z, b = s
-      const double zi = LDS(a + i), si = LDS(b + i);
-      v[s][0] = tail[s] ? zi * zi : 0.0;
-      v[s][1] = tail[s] ? si * si : 0.0;
-      v[s][2] = tail[s] ? zi * si : 0.0;
-    } else if (op == VOP_STEP) {  // scmax(l, a), scmax(l, b)
-      const double li = LDS(LAM + i);
-      v[s][0] = tail[s] ? li * li : (poc[s] ? -LDS(a + i) / li : 0.0);
-      v[s][1] = tail[s] ? li * LDS(a + i) : (poc[s] ? -LDS(b + i) / li : 0.0);
-      v[s][2] = tail[s] ? li * LDS(b + i) : 0.0;
-    } else if (op == VOP_MAXSTEP) {  // max_step(-a), max_step(a)
-      const double xi = LDS(a + i);
-      v[s][0] = tail[s] ? xi * xi : (poc[s] ? xi : 0.0);
-      v[s][1] = poc[s] ? -xi : 0.0;
-    }
-  }
-  if (op == VOP_PAIR || op == VOP_IPROD) nv = 2;
-  if (op == VOP_SCALING || op == VOP_STEP) nv = 3;
-  if (op == VOP_MAXSTEP) nv = 2;
-  pmax = (op == VOP_STEP || op == VOP_MAXSTEP);
-  seg_reduce3(v, nv, pmax, k, nc, ci, ssl, sle, poc);
+  SOCP_SCAN_STEP(0x111, 0xF, rl >= 1 && lane - 1 >= ssl)
+  SOCP_SCAN_STEP(0x112, 0xF, rl >= 2 && lane - 2 >= ssl)
+  SOCP_SCAN_STEP(0x114, 0xF, rl >= 4 && lane - 4 >= ssl)
+  SOCP_SCAN_STEP(0x118, 0xF, rl >= 8 && lane - 8 >= ssl)
+  SOCP_SCAN_STEP(0x142, 0xA, ((lane >> 4) & 1) && ((lane & ~15) - 1 >= ssl))
+  SOCP_SCAN_STEP(0x143, 0xC, lane >= 32 && 31 >= ssl)
+#undef SOCP_SCAN_STEP
+}
 
-  // ---------------- phase 2: outputs
-  if (op == VOP_STEP) {
-    // second round: r2s for both directions; keep the first-round POC maxima
-    double av[2] = {0.0, 0.0}, r1a[2] = {0.0, 0.0}, r1b[2] = {0.0, 0.0}, pm[2];
-    bool dm = false;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int i = 64 * s + lane;
-      const int c = ci[s];
-      pm[s] = poc[s] ? fmax(LDS(O_TOT + c * 4), LDS(O_TOT + c * 4 + 1)) : -INFINITY;
-      v[s][0] = v[s][1] = v[s][2] = 0.0;
-      if (tail[s] || hd[s]) {
-        const int o = eo[s];
-        const double l0 = LDS(LAM + o);
-        const double ai = l0 * l0 - LDS(O_TOT + c * 4);
-        dm |= ai < 0.0;
-        const double aa = 1.0 / sqrt(ai);
-        const double xa0 = LDS(a + o), xb0 = LDS(b + o);
-        const double ra = aa * l0 * xa0 - aa * LDS(O_TOT + c * 4 + 1);
-        const double rb = aa * l0 * xb0 - aa * LDS(O_TOT + c * 4 + 2);
-        av[s] = aa;
-        r1a[s] = ra;
-        r1b[s] = rb;
-        if (tail[s]) {
-          const double csa = (ra + xa0) / (aa * l0 + 1.0);
-          const double csb = (rb + xb0) / (aa * l0 + 1.0);
-          const double li = LDS(LAM + i);
-          const double qa = aa * (LDS(a + i) - csa * aa * li);
-          const double qb = aa * (LDS(b + i) - csb * aa * li);
-          v[s][0] = qa * qa;
-          v[s][1] = qb * qb;
-        }
-      }
-    }
-    SYNC();
-    seg_reduce3(v, 2, false, k, nc, ci, ssl, sle, poc);
-    double best = -INFINITY;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (poc[s]) best = fmax(best, pm[s]);
-      if (hd[s]) {
-        const int c = ci[s];
-        const double va = sqrt(LDS(O_TOT + c * 4)) - av[s] * r1a[s];
-        const double vb = sqrt(LDS(O_TOT + c * 4 + 1)) - av[s] * r1b[s];
-        best = fmax(best, fmax(va, vb));
-      }
-    }
-    double t = wmax(best);
-    if (isnan(t)) t = -INFINITY;
-    t = fmax(t, 0.0);
-    R.r0 = (t == 0.0) ? 1.0 : fmin(1.0, 1.0 / t);
-    R.dom = __any(dm) ? 1 : 0;
-    return R;
+// whole-wave sum / max (scan to lane 63, broadcast through an SGPR)
+__device__ __forceinline__ double wsum(double v) {
+  double x[1] = {v};
+  dpp_scan<1>(x, threadIdx.x, 0, false);
+  return readlane_d(x[0], 63);
+}
+__device__ __forceinline__ double wmax(double v) {
+  double x[1] = {v};
+  dpp_scan<1>(x, threadIdx.x, 0, true);
+  return readlane_d(x[0], 63);
+}
+
+// x^e for an integer exponent (Julia's ^(::Float64, ::Integer); e = 3 is x*x*x)
+__device__ __forceinline__ double ipow(double x, int e) {
+  if (e == 3) return x * x * x;
+  double r = 1.0, b = x;
+  for (int q = e; q > 0; q >>= 1) {
+    if (q & 1) r *= b;
+    b *= b;
   }
-  if (op == VOP_MAXSTEP) {
-    double bm = -INFINITY, bp = -INFINITY;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = ci[s];
-      if (poc[s]) {
-        bm = fmax(bm, LDS(O_TOT + c * 4));
-        bp = fmax(bp, LDS(O_TOT + c * 4 + 1));
-      } else if (hd[s]) {
-        const double nr = sqrt(LDS(O_TOT + c * 4));
-        const double x0 = LDS(a + eo[s]);
-        bm = fmax(bm, nr + x0);
-        bp = fmax(bp, nr - x0);
-      }
-    }
-    R.r0 = wmax(bm);
-    R.r1 = wmax(bp);
-    return R;
-  }
-  bool dm = false;
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    if (!ev[s]) continue;
-    const int i = 64 * s + lane, c = ci[s], o = eo[s];
-    if (op == VOP_SCALE || op == VOP_ISCALE || op == VOP_PAIR) {
-      const double wi = LDS(WB + i), xi = LDS(a + i);
-      double r;
-      if (poc[s]) {
-        r = (op == VOP_ISCALE) ? (1.0 / wi) * xi : wi * xi;
-      } else {
-        const double mu = LDS(O_MU + c), del = LDS(O_TOT + c * 4), wb0 = LDS(WB + o),
-                     x0 = LDS(a + o);
-        if (op != VOP_ISCALE) {
-          const double cst = x0 + del / (1.0 + wb0);
-          r = hd[s] ? mu * (wb0 * x0 + del) : mu * (xi + cst * wi);
-        } else {
-          const double cst = -x0 + del / (1.0 + wb0);
-          const double im = 1.0 / mu;
-          r = hd[s] ? im * (wb0 * x0 - del) : im * (xi + cst * wi);
-        }
-      }
-      if (op == VOP_PAIR) {
-        const double x2 = LDS(b + i);
-        double r2;
-        if (poc[s]) {
-          r2 = (1.0 / wi) * x2;
-        } else {
-          const double mu = LDS(O_MU + c), del = LDS(O_TOT + c * 4 + 1), wb0 = LDS(WB + o),
-                       x0 = LDS(b + o);
-          const double cst = -x0 + del / (1.0 + wb0);
-          const double im = 1.0 / mu;
-          r2 = hd[s] ? im * (wb0 * x0 - del) : im * (x2 + cst * wi);
-        }
-        LDS(o2 + i) = r2;
-      }
-      LDS(o1 + i) = r;
-    } else if (op == VOP_IPROD) {
-      const double vi = LDS(a + i), li = LDS(LAM + i);
-      double r;
-      if (poc[s]) {
-        r = vi / li;
-      } else {
-        const double l0 = LDS(LAM + o), v0 = LDS(a + o);
-        const double aa = l0 * l0 - LDS(O_TOT + c * 4);
-        const double dt = LDS(O_TOT + c * 4 + 1);
-        r = hd[s] ? v0 * l0 / aa - dt / aa : -(v0 * li / aa) + vi / l0 + li * dt / (l0 * aa);
-      }
-      LDS(o1 + i) = r;
-    } else if (op == VOP_VPROD) {
-      const double ui = LDS(a + i), vi = LDS(b + i);
-      double r;
-      if (poc[s])
-        r = ui * vi;
-      else
-        r = hd[s] ? LDS(O_TOT + c * 4) : LDS(a + o) * vi + LDS(b + o) * ui;
-      LDS(o1 + i) = r;
-    } else if (op == VOP_SCALING) {
-      // compute_scaling (scalings.jl:22-99) -> lam, wb, mu, 1/(1+wb0), and
-      // X = W^-1 G row coefficients: X[i,:] = ca[i] G[i,:] + cb[i] U[cone(i),:]
-      const double zi = LDS(a + i), si = LDS(b + i);
-      double wbi, li, cai, cbi;
-      if (poc[s]) {
-        const double r = si / zi, pr = si * zi, ir = zi / si;
-        dm |= (r < 0.0) || (pr < 0.0) || (ir < 0.0);
-        wbi = sqrt(r);
-        li = sqrt(pr);
-        cai = sqrt(ir);
-        cbi = 0.0;
-      } else {
-        const double z0 = LDS(a + o), s0 = LDS(b + o);
-        const double onrmz = z0 * z0 - LDS(O_TOT + c * 4), onrms = s0 * s0 - LDS(O_TOT + c * 4 + 1);
-        dm |= (onrmz < 0.0) || (onrms < 0.0);
-        const double nrmz = sqrt(onrmz), nrms = sqrt(onrms);
-        const double fz = 1.0 / nrmz, fs = 1.0 / nrms;
-        const double zb0 = z0 * fz, sb0 = s0 * fs;
-        const double nsum = zb0 * sb0 + LDS(O_TOT + c * 4 + 2) * fz * fs;
-        const double garg = (1.0 + nsum) / 2.0;
-        dm |= garg < 0.0;
-        const double gamma = sqrt(garg);
-        const double fg = 1.0 / (2.0 * gamma);
-        const double wb0 = (sb0 + zb0) * fg;
-        const double zbi = zi * fz, sbi = si * fs;
-        wbi = hd[s] ? wb0 : (sbi - zbi) * fg;
-        const double ratio = nrms / nrmz, prod = nrms * nrmz;
-        dm |= (ratio < 0.0) || (prod < 0.0);
-        const double mu = sqrt(ratio);
-        const double tmv1 = sqrt(prod);
-        const double mult = tmv1 / (zb0 + sb0 + 2.0 * gamma);
-        li = hd[s] ? gamma * tmv1 : (sbi * (gamma + zb0) + zbi * (gamma + sb0)) * mult;
-        const double im = 1.0 / mu;
-        cai = hd[s] ? -im : im;
-        cbi = hd[s] ? -(1.0 + wb0) * im : wbi * im;
-        if (hd[s]) {
-          LDS(O_MU + c) = mu;
-          LDS(O_I1 + c) = 1.0 / (1.0 + wb0);
-        }
-      }
-      LDS(WB + i) = wbi;
-      LDS(LAM + i) = li;
-      LDS(kv(KV_CA) + i) = cai;
-      LDS(kv(KV_CB) + i) = cbi;
-    }
-  }
-  SYNC();
-  R.dom = __any(dm) ? 1 : 0;
-  return R;
+  return r;
+}
+
+// pivot reciprocal: v_rcp_f64 + two Newton steps (within 1 ulp of 1/d)
+__device__ __forceinline__ double recip(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
 }
 
 // Reduce-scatter over the 16 lanes of a row (xor masks 8,4,2,1): on return the
@@ -494,7 +273,22 @@ struct RSCount<C, 0> {
   static constexpr int value = C;
 };
 
-enum { P_SINGTEST, P_INIT, P_ITER, P_AFFINE, P_COMBINED, P_KKT };
+// cone vector operations (one instance, Small::vop)
+enum : int { VOP_SCALE, VOP_ISCALE, VOP_PAIR, VOP_IPROD, VOP_VPROD, VOP_SCALING, VOP_STEP1,
+             VOP_STEP2, VOP_MAXSTEP };
+
+struct VopResult {
+  double r0, r1;
+  int dom;
+};
+
+// driver micro-phases
+enum : int {
+  MP_SINGTEST, MP_SINGTEST_POST, MP_FACTOR, MP_INIT, MP_INIT_RHS, MP_INIT_POST, MP_INIT_SHIFT,
+  MP_ITER, MP_ITER_B, MP_ITER_C, MP_KKT, MP_KKT_B, MP_KKT_POST,
+  MP_S0, MP_S1, MP_S2, MP_S3, MP_S4, MP_S5, MP_S6, MP_S7,
+  MP_POST_A, MP_POST_B, MP_POST_C, MP_POST_D, MP_AFF_E
+};
 
 template <int NQ, int NP, int MQ>
 struct Small {
@@ -517,19 +311,20 @@ struct Small {
   const int n, m, k, nc;
   bool sing;
   int64_t dbg_p = 0;
+  // compact-layout element info (element i = 64*s + lane): cone, type code
+  // (0 POC, 1 SOC head, 2 SOC tail, 3 none), cone offset, scan segment
+  // start / last lane within the slot
+  int ci[2], kd[2], eo[2], ssl[2], sle[2];
+  STAMP_DECL
 
   AD G[NP][NQ];  // AGPR-resident
   d4 T[NT];
-  d4 AL[NQ * MQ];
+  AD AL[NQ * MQ][4];  // ALi' tiles, AGPR-resident
   d4 Sv[MT];
 
   __device__ __forceinline__ Small(const SmallArgs& args)
       : a(args), lane(threadIdx.x), g(threadIdx.x >> 4), cl(threadIdx.x & 15),
         n(args.n), m(args.m), k(args.k), nc(args.nc) {}
-
-  __device__ __forceinline__ VopResult vop(int op, int x, int y, int o1, int o2) {
-    return cone_vop(op, x, y, o1, o2, k, nc);
-  }
 
   // ---------------------------------------------------------------- setup
   __device__ __forceinline__ void init_tables() {
@@ -552,6 +347,22 @@ struct Small {
       LDS(O_RC + i) = (double)code;
     }
     SYNC();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane;
+      const bool ev = i < k;
+      const int code = ev ? (int)LDS(O_RC + i) : 3;
+      const int c = ev ? (code >> 2) : 0;
+      ci[s] = c;
+      kd[s] = ev ? (code & 3) : 3;
+      const int o = ev ? (int)LDS(O_COFF + c) : i;
+      const int d = ev ? (int)LDS(O_CDIM + c) : 1;
+      eo[s] = o;
+      const int st = o > 64 * s ? o : 64 * s;
+      const int en = (o + d) < 64 * (s + 1) ? (o + d) : 64 * (s + 1);
+      ssl[s] = ev ? st - 64 * s : lane;
+      sle[s] = ev ? en - 1 - 64 * s : -1;
+    }
   }
 
   __device__ __forceinline__ void load_problem(int64_t p) {
@@ -600,6 +411,270 @@ struct Small {
     }
     for (int e = lane; e < NCS * NPAD; e += 64) LDS(O_U + e) = 0.0;
     SYNC();
+  }
+
+  // ------------------------------------------------------ cone vector ops
+  // scale!/iscale! (scalings.jl:112-173), iprod!/vprod! (vectors.jl:58-125),
+  // compute_scaling (scalings.jl:22-99), compute_step/scmax (mats.jl:30-86,
+  // in two rounds STEP1/STEP2), max_step (mats.jl:1-28).  a, b, o1, o2 are
+  // LDS offsets of k-vectors.  Exactly one instance (called from run()).
+  __device__ __forceinline__ VopResult vop(int op, int a_, int b_, int o1, int o2) {
+    double v[2][3];
+    bool mxp = false;
+    int nvals = 1;
+    VopResult R = {0.0, 0.0, 0};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane;
+      const bool tail = kd[s] == 2, hd = kd[s] == 1, poc = kd[s] == 0;
+      double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+      if (op == VOP_SCALE || op == VOP_ISCALE) {
+        if (tail) v0 = LDS(WB + i) * LDS(a_ + i);
+      } else if (op == VOP_PAIR) {
+        if (tail) {
+          v0 = LDS(WB + i) * LDS(a_ + i);
+          v1 = LDS(WB + i) * LDS(b_ + i);
+        }
+      } else if (op == VOP_IPROD) {
+        const double li = LDS(LAM + i);
+        if (tail) {
+          v0 = li * li;
+          v1 = LDS(a_ + i) * li;
+        }
+      } else if (op == VOP_VPROD) {
+        if (tail || hd) v0 = LDS(a_ + i) * LDS(b_ + i);
+      } else if (op == VOP_SCALING) {  // a = z, b = s
+        if (tail) {
+          const double zi = LDS(a_ + i), si = LDS(b_ + i);
+          v0 = zi * zi;
+          v1 = si * si;
+          v2 = zi * si;
+        }
+      } else if (op == VOP_STEP1) {  // scmax(l, a), scmax(l, b): first round
+        const double li = LDS(LAM + i);
+        if (tail) {
+          v0 = li * li;
+          v1 = li * LDS(a_ + i);
+          v2 = li * LDS(b_ + i);
+        } else if (poc) {
+          v0 = -LDS(a_ + i) / li;
+          v1 = -LDS(b_ + i) / li;
+        }
+      } else if (op == VOP_STEP2) {  // second round: r2s of both directions
+        if (tail) {
+          const int o = eo[s], c = ci[s];
+          const double av = LDS(O_CST + c * 4), ra = LDS(O_CST + c * 4 + 1),
+                       rb = LDS(O_CST + c * 4 + 2);
+          const double l0 = LDS(LAM + o), li = LDS(LAM + i);
+          const double csa = (ra + LDS(a_ + o)) / (av * l0 + 1.0);
+          const double csb = (rb + LDS(b_ + o)) / (av * l0 + 1.0);
+          const double qa = av * (LDS(a_ + i) - csa * av * li);
+          const double qb = av * (LDS(b_ + i) - csb * av * li);
+          v0 = qa * qa;
+          v1 = qb * qb;
+        }
+      } else if (op == VOP_MAXSTEP) {  // max_step(-a), max_step(a)
+        const double xi = LDS(a_ + i);
+        if (tail) v0 = xi * xi;
+        if (poc) {
+          v0 = xi;
+          v1 = -xi;
+        }
+      }
+      v[s][0] = v0;
+      v[s][1] = v1;
+      v[s][2] = v2;
+    }
+    if (op == VOP_PAIR || op == VOP_IPROD || op == VOP_STEP2 || op == VOP_MAXSTEP) nvals = 2;
+    if (op == VOP_SCALING || op == VOP_STEP1) nvals = 3;
+    mxp = (op == VOP_STEP1 || op == VOP_MAXSTEP);
+    // ---- per-cone segmented reduction (DPP scan per slot, then per-cone totals)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (64 * s < k) {
+        const bool mx = mxp && kd[s] == 0;
+        if (nvals == 1) {
+          double x[1] = {v[s][0]};
+          dpp_scan<1>(x, lane, ssl[s], mx);
+          v[s][0] = x[0];
+        } else if (nvals == 2) {
+          double x[2] = {v[s][0], v[s][1]};
+          dpp_scan<2>(x, lane, ssl[s], mx);
+          v[s][0] = x[0];
+          v[s][1] = x[1];
+        } else {
+          dpp_scan<3>(v[s], lane, ssl[s], mx);
+        }
+        if (lane == sle[s]) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) LDS(O_PART + (s * NCS + ci[s]) * 4 + q) = v[s][q];
+        }
+      }
+    }
+    SYNC();
+    if (lane < nc) {
+      const int c = lane;
+      const int o = (int)LDS(O_COFF + c), d = (int)LDS(O_CDIM + c);
+      const bool mx = mxp && (int)LDS(O_CKIND + c) == POC_K;
+      const int s0 = o >> 6, s1 = (o + d - 1) >> 6;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        double t = LDS(O_PART + (s0 * NCS + c) * 4 + q);
+        if (s1 > s0) {
+          const double u = LDS(O_PART + (s1 * NCS + c) * 4 + q);
+          t = mx ? fmax(t, u) : t + u;
+        }
+        LDS(O_TOT + c * 4 + q) = t;
+      }
+    }
+    SYNC();
+    // ---- outputs
+    bool dm = false;
+    double best = -INFINITY, bp = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (kd[s] == 3) continue;
+      const int i = 64 * s + lane, c = ci[s], o = eo[s];
+      const bool hd = kd[s] == 1, poc = kd[s] == 0;
+      const double t0 = LDS(O_TOT + c * 4), t1 = LDS(O_TOT + c * 4 + 1), t2 = LDS(O_TOT + c * 4 + 2);
+      if (op == VOP_SCALE || op == VOP_ISCALE || op == VOP_PAIR) {
+        const double wi = LDS(WB + i), xi = LDS(a_ + i);
+        double r;
+        if (poc) {
+          r = (op == VOP_ISCALE) ? (1.0 / wi) * xi : wi * xi;
+        } else {
+          const double mu = LDS(O_MU + c), wb0 = LDS(WB + o), x0 = LDS(a_ + o);
+          if (op != VOP_ISCALE) {
+            const double cst = x0 + t0 / (1.0 + wb0);
+            r = hd ? mu * (wb0 * x0 + t0) : mu * (xi + cst * wi);
+          } else {
+            const double cst = -x0 + t0 / (1.0 + wb0);
+            const double im = 1.0 / mu;
+            r = hd ? im * (wb0 * x0 - t0) : im * (xi + cst * wi);
+          }
+        }
+        if (op == VOP_PAIR) {
+          const double x2 = LDS(b_ + i);
+          double r2;
+          if (poc) {
+            r2 = (1.0 / wi) * x2;
+          } else {
+            const double mu = LDS(O_MU + c), wb0 = LDS(WB + o), x0 = LDS(b_ + o);
+            const double cst = -x0 + t1 / (1.0 + wb0);
+            const double im = 1.0 / mu;
+            r2 = hd ? im * (wb0 * x0 - t1) : im * (x2 + cst * wi);
+          }
+          LDS(o2 + i) = r2;
+        }
+        LDS(o1 + i) = r;
+      } else if (op == VOP_IPROD) {
+        const double vi = LDS(a_ + i), li = LDS(LAM + i);
+        double r;
+        if (poc) {
+          r = vi / li;
+        } else {
+          const double l0 = LDS(LAM + o), v0 = LDS(a_ + o);
+          const double aa = l0 * l0 - t0;
+          r = hd ? v0 * l0 / aa - t1 / aa : -(v0 * li / aa) + vi / l0 + li * t1 / (l0 * aa);
+        }
+        LDS(o1 + i) = r;
+      } else if (op == VOP_VPROD) {
+        const double ui = LDS(a_ + i), vi = LDS(b_ + i);
+        double r;
+        if (poc)
+          r = ui * vi;
+        else
+          r = hd ? t0 : LDS(a_ + o) * vi + LDS(b_ + o) * ui;
+        LDS(o1 + i) = r;
+      } else if (op == VOP_SCALING) {
+        // compute_scaling (scalings.jl:22-99) -> lam, wb, mu, 1/(1+wb0), and the
+        // X = W^-1 G row coefficients: X[i,:] = ca[i] G[i,:] + cb[i] U[cone(i),:]
+        const double zi = LDS(a_ + i), si = LDS(b_ + i);
+        double wbi, li, cai, cbi;
+        if (poc) {
+          const double r = si / zi, pr = si * zi, ir = zi / si;
+          dm |= (r < 0.0) || (pr < 0.0) || (ir < 0.0);
+          wbi = sqrt(r);
+          li = sqrt(pr);
+          cai = sqrt(ir);
+          cbi = 0.0;
+        } else {
+          const double z0 = LDS(a_ + o), s0 = LDS(b_ + o);
+          const double onrmz = z0 * z0 - t0, onrms = s0 * s0 - t1;
+          dm |= (onrmz < 0.0) || (onrms < 0.0);
+          const double nrmz = sqrt(onrmz), nrms = sqrt(onrms);
+          const double fz = 1.0 / nrmz, fs = 1.0 / nrms;
+          const double zb0 = z0 * fz, sb0 = s0 * fs;
+          const double nsum = zb0 * sb0 + t2 * fz * fs;
+          const double garg = (1.0 + nsum) / 2.0;
+          dm |= garg < 0.0;
+          const double gamma = sqrt(garg);
+          const double fg = 1.0 / (2.0 * gamma);
+          const double wb0 = (sb0 + zb0) * fg;
+          const double zbi = zi * fz, sbi = si * fs;
+          wbi = hd ? wb0 : (sbi - zbi) * fg;
+          const double ratio = nrms / nrmz, prod = nrms * nrmz;
+          dm |= (ratio < 0.0) || (prod < 0.0);
+          const double mu = sqrt(ratio);
+          const double tmv1 = sqrt(prod);
+          const double mult = tmv1 / (zb0 + sb0 + 2.0 * gamma);
+          li = hd ? gamma * tmv1 : (sbi * (gamma + zb0) + zbi * (gamma + sb0)) * mult;
+          const double im = 1.0 / mu;
+          cai = hd ? -im : im;
+          cbi = hd ? -(1.0 + wb0) * im : wbi * im;
+          if (hd) {
+            LDS(O_MU + c) = mu;
+            LDS(O_I1 + c) = 1.0 / (1.0 + wb0);
+          }
+        }
+        LDS(WB + i) = wbi;
+        LDS(LAM + i) = li;
+        LDS(CA + i) = cai;
+        LDS(CBV + i) = cbi;
+      } else if (op == VOP_STEP1) {
+        if (hd) {
+          const double l0 = LDS(LAM + o);
+          const double ai = l0 * l0 - t0;
+          dm |= ai < 0.0;
+          const double av = 1.0 / sqrt(ai);
+          LDS(O_CST + c * 4) = av;
+          LDS(O_CST + c * 4 + 1) = av * l0 * LDS(a_ + o) - av * t1;
+          LDS(O_CST + c * 4 + 2) = av * l0 * LDS(b_ + o) - av * t2;
+        } else if (poc && i == o) {
+          LDS(O_CST + c * 4 + 3) = fmax(t0, t1);
+        }
+      } else if (op == VOP_STEP2) {
+        if (hd) {
+          const double av = LDS(O_CST + c * 4);
+          const double va = sqrt(t0) - av * LDS(O_CST + c * 4 + 1);
+          const double vb = sqrt(t1) - av * LDS(O_CST + c * 4 + 2);
+          best = fmax(best, fmax(va, vb));
+        } else if (poc && i == o) {
+          best = fmax(best, LDS(O_CST + c * 4 + 3));
+        }
+      } else if (op == VOP_MAXSTEP) {
+        if (poc && i == o) {
+          best = fmax(best, t0);
+          bp = fmax(bp, t1);
+        } else if (hd) {
+          const double nr = sqrt(t0), x0 = LDS(a_ + o);
+          best = fmax(best, nr + x0);
+          bp = fmax(bp, nr - x0);
+        }
+      }
+    }
+    SYNC();
+    R.dom = __any(dm) ? 1 : 0;
+    if (op == VOP_STEP2) {
+      double t = wmax(best);
+      if (isnan(t)) t = -INFINITY;
+      t = fmax(t, 0.0);
+      R.r0 = (t == 0.0) ? 1.0 : fmin(1.0, 1.0 / t);
+    } else if (op == VOP_MAXSTEP) {
+      R.r0 = wmax(best);
+      R.r1 = wmax(bp);
+    }
+    return R;
   }
 
   // U[c,:] = (sum_{i in cone c} w_i G[i,:]) / (1+wb0), w_head = -(1+wb0), w_tail = wb_i
@@ -699,16 +774,15 @@ struct Small {
       SYNC();
       const double d = LDS(cb + p);
       if (!(d > 0.0)) return false;
-      const double rinv = 1.0 / d;
-      double cR[Q][4], cC[Q];
+      const double rinv = recip(d);
+      double cC[Q];
+#pragma unroll
+      for (int ti = 0; ti < Q; ++ti) cC[ti] = LDS(cb + 16 * ti + cl) * rinv;
 #pragma unroll
       for (int ti = 0; ti < Q; ++ti) {
+        double cR[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cR[ti][r] = LDS(cb + 16 * ti + g + 4 * r);
-        cC[ti] = LDS(cb + 16 * ti + cl) * rinv;
-      }
-#pragma unroll
-      for (int ti = 0; ti < Q; ++ti)
+        for (int r = 0; r < 4; ++r) cR[r] = LDS(cb + 16 * ti + g + 4 * r);
 #pragma unroll
         for (int tj = 0; tj <= ti; ++tj) {
           d4& t = M[tri(ti, tj)];
@@ -717,18 +791,19 @@ struct Small {
             for (int r = 0; r < 4; ++r) {
               const int R = 16 * ti + g + 4 * r, Cc = 16 * tj + cl;
               const bool iR = R == p, iC = Cc == p;
-              const double gen = fma(-cR[ti][r], cC[tj], t[r]);
+              const double gen = fma(-cR[r], cC[tj], t[r]);
               // pivot row and column both come from the gathered column p:
               // re-symmetrising them every step is what keeps the sweep's
               // inverse a good right-inverse at kappa ~ 1e10.
-              const double scol = cR[ti][r] * rinv;
+              const double scol = cR[r] * rinv;
               t[r] = (iR && iC) ? -rinv : (iC ? scol : (iR ? cC[tj] : gen));
             }
           } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) t[r] = fma(-cR[ti][r], cC[tj], t[r]);
+            for (int r = 0; r < 4; ++r) t[r] = fma(-cR[r], cC[tj], t[r]);
           }
         }
+      }
     }
     return true;
   }
@@ -761,12 +836,18 @@ struct Small {
 
   // H (+A'A) -> sweep -> Li;  ALi' = Li A' (n x m);  S = A ALi';  S^-1.
   __device__ __forceinline__ int factor(bool identity, bool addAA) {
+    STAMP(SP_OTHER);
     if (!identity) compute_U();
+    STAMP(SP_U);
     form_H(addAA);
     SYNC();
-    double* dbg = (a.dbg && a.mode == MODE_KKT) ? a.dbg + dbg_p * (int64_t)(2 * n * n + 2 * k) : nullptr;
+    STAMP(SP_SYRK);
+    // debug dump per problem: H, -H^-1 (n x n each), lam, wbar (k each), ALi' (n x m), S (m x m)
+    double* dbg = (a.dbg && a.mode == MODE_KKT) ? a.dbg + dbg_p * (int64_t)(2 * n * n + 2 * k + n * m + m * m) : nullptr;
     if (dbg) dump_sym(dbg);
-    if (!sweep<NQ>(T, n)) return ST_CHOL_H;
+    const bool okH = sweep<NQ>(T, n);
+    STAMP(SP_SWEEP_H);
+    if (!okH) return ST_CHOL_H;
 #pragma unroll
     for (int t = 0; t < NT; ++t) T[t] = -T[t];
     if (dbg) {
@@ -795,7 +876,9 @@ struct Small {
             acc[tm] = mfma(Ut[s], LDS(O_A + (16 * tm + cl) * LDA + 16 * tk + g + 4 * s), acc[tm]);
       }
 #pragma unroll
-      for (int tm = 0; tm < MQ; ++tm) AL[ti * MQ + tm] = acc[tm];
+      for (int tm = 0; tm < MQ; ++tm)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a_put(AL[ti * MQ + tm][r], acc[tm][r]);
     }
 #pragma unroll
     for (int tm = 0; tm < MQ; ++tm)
@@ -806,7 +889,7 @@ struct Small {
         for (int tk = 0; tk < NQ; ++tk)
 #pragma unroll
           for (int s = 0; s < 4; ++s)
-            acc = mfma(LDS(O_A + (16 * tm + cl) * LDA + 16 * tk + g + 4 * s), AL[tk * MQ + tq][s], acc);
+            acc = mfma(LDS(O_A + (16 * tm + cl) * LDA + 16 * tk + g + 4 * s), a_get_mfma(AL[tk * MQ + tq][s]), acc);
         Sv[tri(tm, tq)] = acc;
       }
 #pragma unroll
@@ -816,54 +899,82 @@ struct Small {
         const int R = 16 * tm + g + 4 * r, Cc = 16 * tm + cl;
         if (R == Cc && R >= m) Sv[tri(tm, tm)][r] = 1.0;
       }
+    if (dbg) {
+      double* dA = dbg + 2 * n * n + 2 * k;
+      double* dS = dA + n * m;
+#pragma unroll
+      for (int ti = 0; ti < NQ; ++ti)
+#pragma unroll
+        for (int tm = 0; tm < MQ; ++tm)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int R = 16 * ti + g + 4 * r, Cc = 16 * tm + cl;
+            const double v = a_get(AL[ti * MQ + tm][r]);
+            if (R < n && Cc < m) dA[R * m + Cc] = v;
+          }
+#pragma unroll
+      for (int tm = 0; tm < MQ; ++tm)
+#pragma unroll
+        for (int tq = 0; tq <= tm; ++tq)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int R = 16 * tm + g + 4 * r, Cc = 16 * tq + cl;
+            if (R < m && Cc < m) dS[R * m + Cc] = Sv[tri(tm, tq)][r];
+          }
+    }
     SYNC();
-    if (!sweep<MQ>(Sv, m)) return ST_CHOL_S;
+    const bool okS = sweep<MQ>(Sv, m);
+    STAMP(SP_SCHUR);
+    if (!okS) return ST_CHOL_S;
 #pragma unroll
     for (int t = 0; t < MT; ++t) Sv[t] = -Sv[t];
     return 0;
   }
 
-  // out = M*v for a symmetric matrix stored as lower tiles (C/D layout)
+  // out = M*v for a symmetric matrix stored as lower tiles (C/D layout).
+  // Lower part: per tile row, reduce over the 16 column lanes; strictly upper
+  // part (transposed off-diagonal tiles): reduce over the 4 row groups.
   template <int Q>
   __device__ __forceinline__ void symv(const d4 (&M)[Q * (Q + 1) / 2], int vin, int vout) {
-    double vc[Q], vr[Q][4];
+    double vc[Q], P2[Q];
 #pragma unroll
     for (int t = 0; t < Q; ++t) {
       vc[t] = LDS(vin + 16 * t + cl);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) vr[t][r] = LDS(vin + 16 * t + g + 4 * r);
+      P2[t] = 0.0;
     }
-    double P1[4 * Q], P2[Q];
+    double P1row[Q];
 #pragma unroll
-    for (int t = 0; t < Q; ++t) P2[t] = 0.0;
-#pragma unroll
-    for (int ti = 0; ti < Q; ++ti)
+    for (int ti = 0; ti < Q; ++ti) {
+      double vr[4], P1[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        vr[r] = LDS(vin + 16 * ti + g + 4 * r);
         double acc = 0.0;
 #pragma unroll
         for (int tj = 0; tj <= ti; ++tj) acc = fma(M[tri(ti, tj)][r], vc[tj], acc);
-        P1[ti * 4 + r] = acc;
+        P1[r] = acc;
       }
-#pragma unroll
-    for (int ti = 0; ti < Q; ++ti)
 #pragma unroll
       for (int tj = 0; tj < ti; ++tj)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) P2[tj] = fma(M[tri(ti, tj)][r], vr[ti][r], P2[tj]);
-    int base = 0;
-    rs16<4 * Q, 8>(P1, cl, base);
-    constexpr int CF = RSCount<4 * Q, 8>::value;
+        for (int r = 0; r < 4; ++r) P2[tj] = fma(M[tri(ti, tj)][r], vr[r], P2[tj]);
+      int base = 0;
+      rs16<4, 8>(P1, cl, base);  // one value per lane: row 16ti + g + 4*base
+      P1row[ti] = P1[0] + 0.0 * base;
+      // stash the row index in base via the lane's own cl bits (see write below)
+    }
 #pragma unroll
     for (int t = 0; t < Q; ++t) {
       P2[t] += __shfl_xor(P2[t], 16);
       P2[t] += __shfl_xor(P2[t], 32);
     }
     SYNC();
+    {
+      // rs16<4,8>: bit 8 of cl picks entries 2-3, bit 4 picks the odd one; masks
+      // 2 and 1 are all-reduce steps, so the lane holds entry (cl>>3&1)*2 + (cl>>2&1)
+      const int r = ((cl >> 3) & 1) * 2 + ((cl >> 2) & 1);
 #pragma unroll
-    for (int j = 0; j < CF; ++j) {
-      const int idx = base + j;
-      LDS(vout + 16 * (idx >> 2) + g + 4 * (idx & 3)) = P1[j];
+      for (int ti = 0; ti < Q; ++ti) LDS(vout + 16 * ti + g + 4 * r) = P1row[ti];
     }
     SYNC();
     if (g == 0) {
@@ -939,65 +1050,6 @@ struct Small {
     return acc;
   }
 
-  // ------------------------------------------------------------ KKT solve
-  // solve_kkt(::DenseSolver) (densesolver.jl:54-90) for (RD,RP,DZ,DS) ->
-  // (RX,RY,RZ,RS).  init selects m0 = -cy (exact elimination) for the W = I
-  // initial-point system; otherwise the reference's sing branch is kept.
-  __device__ __forceinline__ void solve(bool init) {
-    vop(VOP_IPROD, DS, 0, K0, 0);              // k0 = lam^-1 o ds
-    vop(VOP_SCALE, K0, 0, K1, 0);              // k1 = W k0
-    for (int i = lane; i < k; i += 64) LDS(K2 + i) = LDS(DZ + i) - LDS(K1 + i);
-    SYNC();
-    vop(VOP_ISCALE, K2, 0, T1, 0);
-    vop(VOP_ISCALE, T1, 0, T2, 0);             // t2 = iWiW k2
-    double acc[NQ];
-    gemv_Gt(T2, acc);                          // GWiWi*k2 = G'(W^-2 k2)
-    if (g == 0) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) LDS(TN + 16 * q + cl) = acc[q];
-    }
-    SYNC();
-    if (lane < n) {
-      double v = LDS(TN + lane) + LDS(RD + lane);
-      if (sing) v = v + At_times(RP, lane);
-      LDS(N0 + lane) = v;
-    }
-    SYNC();
-    {  // m0 = ALi*n0 - dy
-      double vr[NQ][4];
-#pragma unroll
-      for (int t = 0; t < NQ; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) vr[t][r] = LDS(N0 + 16 * t + g + 4 * r);
-#pragma unroll
-      for (int tm = 0; tm < MQ; ++tm) {
-        double pacc = 0.0;
-#pragma unroll
-        for (int ti = 0; ti < NQ; ++ti)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pacc = fma(AL[ti * MQ + tm][r], vr[ti][r], pacc);
-        pacc += __shfl_xor(pacc, 16);
-        pacc += __shfl_xor(pacc, 32);
-        const int i = 16 * tm + cl;
-        if (g == 0 && i < m) LDS(M0 + i) = pacc - LDS(RP + i);
-      }
-    }
-    SYNC();
-    symv<MQ>(Sv, M0, RY);                      // cy = S^-1 m0
-    if (lane < m) LDS(M0 + lane) = (sing && !init) ? LDS(RP + lane) - LDS(RY + lane) : -LDS(RY + lane);
-    SYNC();
-    if (lane < n) LDS(N0 + lane) = LDS(N0 + lane) + At_times(M0, lane);
-    SYNC();
-    symv<NQ>(T, N0, RX);                       // cx = Li n0
-    gemv_G(RX, -1, K2, K1);                    // k1 = G cx - k2
-    vop(VOP_ISCALE, K1, 0, T1, 0);
-    vop(VOP_ISCALE, T1, 0, RZ, 0);             // cz = iWiW k1
-    vop(VOP_SCALE, RZ, 0, K1, 0);              // k1 = W cz
-    for (int i = lane; i < k; i += 64) LDS(K0 + i) = LDS(K0 + i) - LDS(K1 + i);
-    SYNC();
-    vop(VOP_SCALE, K0, 0, RS, 0);              // cs = W k0
-  }
-
   // rd = A'y + G'z + c, rp = Ax - b, rz = Gx + s - h (solver.jl:109-118)
   __device__ __forceinline__ void residuals(double& nd, double& np_, double& gap) {
     double acc[NQ];
@@ -1025,14 +1077,66 @@ struct Small {
     gap = wsum(zs);
   }
 
+  // The matrix part of solve_kkt(::DenseSolver) (densesolver.jl:66-85), between
+  // the cone ops: n0 = GWiWi*k2 + dx (+A'dy if sing); m0 = ALi*n0 - dy;
+  // cy = S^-1 m0; m0 = sing ? dy - cy : -cy (init: -cy); n0 += A'm0;
+  // cx = Li n0; k1 = G cx - k2.   In: RD RP T2(=W^-2 k2) K2.  Out: RX RY K1.
+  __device__ __forceinline__ void solve_matrix_part(bool init) {
+    double acc[NQ];
+    gemv_Gt(T2, acc);
+    if (g == 0) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) LDS(TN + 16 * q + cl) = acc[q];
+    }
+    SYNC();
+    if (lane < n) {
+      double v = LDS(TN + lane) + LDS(RD + lane);
+      if (sing) v = v + At_times(RP, lane);
+      LDS(N0 + lane) = v;
+    }
+    SYNC();
+    {
+      double vr[NQ][4];
+#pragma unroll
+      for (int t = 0; t < NQ; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) vr[t][r] = LDS(N0 + 16 * t + g + 4 * r);
+#pragma unroll
+      for (int tm = 0; tm < MQ; ++tm) {
+        double pacc = 0.0;
+#pragma unroll
+        for (int ti = 0; ti < NQ; ++ti)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pacc = fma(a_get(AL[ti * MQ + tm][r]), vr[ti][r], pacc);
+        pacc += __shfl_xor(pacc, 16);
+        pacc += __shfl_xor(pacc, 32);
+        const int i = 16 * tm + cl;
+        if (g == 0 && i < m) LDS(M0 + i) = pacc - LDS(RP + i);
+      }
+    }
+    SYNC();
+    symv<MQ>(Sv, M0, RY);
+    if (lane < m) LDS(M0 + lane) = (sing && !init) ? LDS(RP + lane) - LDS(RY + lane) : -LDS(RY + lane);
+    SYNC();
+    if (lane < n) LDS(N0 + lane) = LDS(N0 + lane) + At_times(M0, lane);
+    SYNC();
+    symv<NQ>(T, N0, RX);
+    gemv_G(RX, -1, K2, K1);
+  }
+
   // ------------------------------------------------------------- driver
+  // solve_socp (solver.jl:40-153) as a micro-phase loop; solve_kkt
+  // (densesolver.jl:54-90) is phases MP_S0..MP_S7, returning to `ret`.
   __device__ __forceinline__ void run(int64_t p) {
+    STAMP(SP_LOAD);
     dbg_p = p;
     int status = ST_MAXIT, iters = 0, it = 0;
     double nd = NAN, np_ = NAN, gap = NAN;
-    double sig = 0.0, mu_ipm = 0.0;
-    int phase;
+    double sig = 0.0, mu_ipm = 0.0, tstep = 0.0;
+    bool fac_ident = false, fac_aa = false, dom_step = false;
+    int fret = 0, ret = 0, fst = 0;
     int after_singtest;
+    VopResult vr = {0.0, 0.0, 0};
     if (a.mode == MODE_KKT) {
       for (int i = lane; i < k; i += 64) {
         LDS(S_ + i) = a.s[p * k + i];
@@ -1042,7 +1146,7 @@ struct Small {
       }
       for (int j = lane; j < n; j += 64) LDS(RD + j) = a.dx[p * n + j];
       for (int i = lane; i < m; i += 64) LDS(RP + i) = a.dy[p * m + i];
-      after_singtest = P_KKT;
+      after_singtest = MP_KKT;
     } else if (a.flags & F_WARM) {
       for (int j = lane; j < n; j += 64) LDS(X_ + j) = a.x[p * n + j];
       for (int i = lane; i < m; i += 64) LDS(Y_ + i) = a.y[p * m + i];
@@ -1050,60 +1154,51 @@ struct Small {
         LDS(Z_ + i) = a.z[p * k + i];
         LDS(S_ + i) = a.s[p * k + i];
       }
-      after_singtest = P_ITER;
+      after_singtest = MP_ITER;
     } else {
-      after_singtest = P_INIT;
+      after_singtest = MP_INIT;
     }
     SYNC();
+    int phase;
     if (a.sing) {
       sing = a.sing[p] != 0;
       phase = after_singtest;
     } else {
       sing = false;
-      phase = P_SINGTEST;
+      phase = MP_SINGTEST;
     }
-    while (true) {
-      // ------------------------------------------------ stage 1: factor
-      if (phase != P_COMBINED) {
-        bool ident = phase == P_SINGTEST || phase == P_INIT;
-        if (ident) {
+    bool done = false;
+    while (!done) {
+      int op = -1, va = 0, vb = 0, vo1 = 0, vo2 = 0;
+      int next = phase;
+      switch (phase) {
+        case MP_SINGTEST:  // Problem's `sing` (Socp.jl:49-56): is G'G positive definite?
           scaling_identity();
-        } else {
-          if (phase == P_ITER) {
-            residuals(nd, np_, gap);
-            if (it >= a.maxit) break;
-          }
-          VopResult sr = vop(VOP_SCALING, Z_, S_, 0, 0);
-          if (sr.dom) {
-            status = ST_DOMAIN;
-            break;
-          }
-          if (phase == P_ITER) {
-            vop(VOP_VPROD, LAM, LAM, DS, 0);     // ds = lam o lam
-            if (nd + np_ + gap < a.tol) {
-              status = ST_CONVERGED;
-              break;
-            }
-            for (int j = lane; j < n; j += 64) LDS(RD + j) = -LDS(RD + j);
-            for (int i = lane; i < m; i += 64) LDS(RP + i) = -LDS(RP + i);
-            for (int i = lane; i < k; i += 64) {
-              LDS(DZ + i) = -LDS(DZ + i);
-              LDS(DS + i) = -LDS(DS + i);
-            }
-            SYNC();
-          }
-        }
-        const int st = factor(ident, phase == P_SINGTEST ? false : sing);
-        if (phase == P_SINGTEST) {
-          sing = (st == ST_CHOL_H);
-          phase = after_singtest;
-          continue;
-        }
-        if (st) {
-          status = st;
+          fac_ident = true;
+          fac_aa = false;
+          fret = MP_SINGTEST_POST;
+          next = MP_FACTOR;
           break;
-        }
-        if (phase == P_INIT) {
+        case MP_SINGTEST_POST:
+          sing = (fst == ST_CHOL_H);
+          next = after_singtest;
+          break;
+        case MP_FACTOR:  // setup_iter (densesolver.jl:41-52)
+          fst = factor(fac_ident, fac_aa);
+          if (fst && fret != MP_SINGTEST_POST) {
+            status = fst;
+            done = true;
+          }
+          next = fret;
+          break;
+        case MP_INIT:  // initial point: the KKT system with W = I (solver.jl:68-84)
+          scaling_identity();
+          fac_ident = true;
+          fac_aa = sing;
+          fret = MP_INIT_RHS;
+          next = MP_FACTOR;
+          break;
+        case MP_INIT_RHS:
           for (int j = lane; j < n; j += 64) LDS(RD + j) = -LDS(C_ + j);
           for (int i = lane; i < m; i += 64) LDS(RP + i) = LDS(B_ + i);
           for (int i = lane; i < k; i += 64) {
@@ -1111,84 +1206,250 @@ struct Small {
             LDS(DS + i) = 0.0;
           }
           SYNC();
+          ret = MP_INIT_POST;
+          next = MP_S0;
+          break;
+        case MP_INIT_POST:
+          op = VOP_MAXSTEP;
+          va = RZ;
+          next = MP_INIT_SHIFT;
+          break;
+        case MP_INIT_SHIFT: {  // cone shift (solver.jl:86-104)
+          const double alphp = vr.r0, alphd = vr.r1;  // max_step(-iz), max_step(iz)
+          for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(RX + j);
+          for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(RY + i);
+          for (int i = lane; i < k; i += 64) {
+            const double iz = LDS(RZ + i), e = e_of(i);
+            LDS(S_ + i) = (fabs(alphp) < a.init_eps) ? -iz : -iz + (1.0 + alphp) * e;
+            LDS(Z_ + i) = (fabs(alphd) < a.init_eps) ? iz : iz + (1.0 + alphd) * e;
+          }
+          SYNC();
+          next = MP_ITER;
+          break;
         }
-        if (phase == P_ITER) phase = P_AFFINE;
-      }
-      // ------------------------------------------------ stage 2: solve
-      solve(phase == P_INIT);
-      // ------------------------------------------------ stage 3: use it
-      if (phase == P_KKT) {
-        status = 0;
-        for (int j = lane; j < n; j += 64) a.cx[p * n + j] = LDS(RX + j);
-        for (int i = lane; i < m; i += 64) a.cy[p * m + i] = LDS(RY + i);
-        for (int i = lane; i < k; i += 64) {
-          a.cz[p * k + i] = LDS(RZ + i);
-          a.cs[p * k + i] = LDS(RS + i);
+        case MP_ITER:  // residuals (solver.jl:109-118), then compute_scaling (:106)
+          STAMP(SP_OTHER);
+          residuals(nd, np_, gap);
+          STAMP(SP_RESID);
+          if (it >= a.maxit) {
+            done = true;
+            break;
+          }
+          op = VOP_SCALING;
+          va = Z_;
+          vb = S_;
+          next = MP_ITER_B;
+          break;
+        case MP_ITER_B:
+          if (vr.dom) {
+            status = ST_DOMAIN;
+            done = true;
+            break;
+          }
+          op = VOP_VPROD;  // ds = lam o lam (solver.jl:120)
+          va = LAM;
+          vb = LAM;
+          vo1 = DS;
+          next = MP_ITER_C;
+          break;
+        case MP_ITER_C:
+          if (nd + np_ + gap < a.tol) {  // exit test (solver.jl:122)
+            status = ST_CONVERGED;
+            done = true;
+            break;
+          }
+          for (int j = lane; j < n; j += 64) LDS(RD + j) = -LDS(RD + j);
+          for (int i = lane; i < m; i += 64) LDS(RP + i) = -LDS(RP + i);
+          for (int i = lane; i < k; i += 64) {
+            LDS(DZ + i) = -LDS(DZ + i);
+            LDS(DS + i) = -LDS(DS + i);
+          }
+          SYNC();
+          fac_ident = false;
+          fac_aa = sing;
+          fret = MP_S0;
+          ret = MP_POST_A;
+          dom_step = false;
+          next = MP_FACTOR;
+          break;
+        case MP_KKT:
+          op = VOP_SCALING;
+          va = Z_;
+          vb = S_;
+          next = MP_KKT_B;
+          break;
+        case MP_KKT_B:
+          if (vr.dom) {
+            status = ST_DOMAIN;
+            done = true;
+            break;
+          }
+          fac_ident = false;
+          fac_aa = sing;
+          fret = MP_S0;
+          ret = MP_KKT_POST;
+          next = MP_FACTOR;
+          break;
+        case MP_KKT_POST:
+          status = 0;
+          for (int j = lane; j < n; j += 64) a.cx[p * n + j] = LDS(RX + j);
+          for (int i = lane; i < m; i += 64) a.cy[p * m + i] = LDS(RY + i);
+          for (int i = lane; i < k; i += 64) {
+            a.cz[p * k + i] = LDS(RZ + i);
+            a.cs[p * k + i] = LDS(RS + i);
+          }
+          done = true;
+          break;
+        // ------------------------------- solve_kkt (densesolver.jl:54-90)
+        case MP_S0:
+          STAMP(SP_OTHER);
+          op = VOP_IPROD;  // k0 = lam^-1 o ds
+          va = DS;
+          vo1 = K0;
+          next = MP_S1;
+          break;
+        case MP_S1:
+          op = VOP_SCALE;  // k1 = W k0
+          va = K0;
+          vo1 = K1;
+          next = MP_S2;
+          break;
+        case MP_S2:
+          for (int i = lane; i < k; i += 64) LDS(K2 + i) = LDS(DZ + i) - LDS(K1 + i);
+          SYNC();
+          op = VOP_ISCALE;
+          va = K2;
+          vo1 = T1;
+          next = MP_S3;
+          break;
+        case MP_S3:
+          op = VOP_ISCALE;  // t2 = iWiW k2
+          va = T1;
+          vo1 = T2;
+          next = MP_S4;
+          break;
+        case MP_S4:
+          STAMP(SP_VOP);
+          solve_matrix_part(ret == MP_INIT_POST);
+          STAMP(SP_SOLVE);
+          op = VOP_ISCALE;
+          va = K1;
+          vo1 = T1;
+          next = MP_S5;
+          break;
+        case MP_S5:
+          op = VOP_ISCALE;  // cz = iWiW k1
+          va = T1;
+          vo1 = RZ;
+          next = MP_S6;
+          break;
+        case MP_S6:
+          op = VOP_SCALE;  // k1 = W cz
+          va = RZ;
+          vo1 = K1;
+          next = MP_S7;
+          break;
+        case MP_S7:
+          for (int i = lane; i < k; i += 64) LDS(K0 + i) = LDS(K0 + i) - LDS(K1 + i);
+          SYNC();
+          op = VOP_SCALE;  // cs = W k0
+          va = K0;
+          vo1 = RS;
+          next = ret;
+          break;
+        // ------------------- step length (solver.jl:128-134, 143-146)
+        case MP_POST_A:
+          STAMP(SP_VOP);
+          op = VOP_PAIR;  // kt3 = W rz, kt2 = W^-1 rs
+          va = RZ;
+          vb = RS;
+          vo1 = T1;
+          vo2 = T2;
+          next = MP_POST_B;
+          break;
+        case MP_POST_B:
+          op = VOP_STEP1;
+          va = T1;
+          vb = T2;
+          next = MP_POST_C;
+          break;
+        case MP_POST_C:
+          dom_step = vr.dom != 0;
+          op = VOP_STEP2;
+          va = T1;
+          vb = T2;
+          next = MP_POST_D;
+          break;
+        case MP_POST_D: {
+          if (dom_step) {
+            status = ST_DOMAIN;
+            done = true;
+            break;
+          }
+          tstep = vr.r0;
+          if (ret == MP_POST_A) {  // affine direction -> centering + corrector
+            double kk = 0.0, ll = 0.0;
+            for (int i = lane; i < k; i += 64) {
+              kk += LDS(T2 + i) * LDS(T1 + i);
+              ll += LDS(LAM + i) * LDS(LAM + i);
+            }
+            kk = wsum(kk);
+            ll = wsum(ll);
+            const double t = tstep;
+            const double rho = 1.0 - t - t * t * kk / ll;
+            const double cr = isnan(rho) ? rho : (rho < 0.0 ? 0.0 : (rho > 1.0 ? 1.0 : rho));
+            sig = ipow(cr, a.sigma_exp);  // max(0,min(1,rho))^3 (solver.jl:133)
+            mu_ipm = ll / a.deg;
+            op = VOP_VPROD;  // kt1 = kt2 o kt3
+            va = T2;
+            vb = T1;
+            vo1 = K0;
+            next = MP_AFF_E;
+          } else {  // combined direction -> step and update (solver.jl:143-150)
+            const double stp = tstep * a.step;
+            for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(X_ + j) + LDS(RX + j) * stp;
+            for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(Y_ + i) + LDS(RY + i) * stp;
+            for (int i = lane; i < k; i += 64) {
+              LDS(Z_ + i) = LDS(Z_ + i) + LDS(RZ + i) * stp;
+              LDS(S_ + i) = LDS(S_ + i) + LDS(RS + i) * stp;
+            }
+            SYNC();
+            STAMP(SP_STEP);
+            iters = ++it;
+            next = MP_ITER;
+          }
+          break;
         }
-        break;
-      }
-      if (phase == P_INIT) {
-        // initial point and cone shift (solver.jl:84-104)
-        const VopResult ms = vop(VOP_MAXSTEP, RZ, 0, 0, 0);
-        const double alphp = ms.r0, alphd = ms.r1;  // max_step(-iz), max_step(iz)
-        for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(RX + j);
-        for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(RY + i);
-        for (int i = lane; i < k; i += 64) {
-          const double iz = LDS(RZ + i), e = e_of(i);
-          LDS(S_ + i) = (fabs(alphp) < a.init_eps) ? -iz : -iz + (1.0 + alphp) * e;
-          LDS(Z_ + i) = (fabs(alphd) < a.init_eps) ? iz : iz + (1.0 + alphd) * e;
+        case MP_AFF_E: {  // ds += sig*mu*e - kt2 o kt3; dx,dy,dz *= 1-sig (solver.jl:136-140)
+          const double scf = 1.0 - sig;
+          for (int i = lane; i < k; i += 64) {
+            const double kt2 = sig * mu_ipm * e_of(i);
+            LDS(DS + i) = LDS(DS + i) + (kt2 - LDS(K0 + i));
+            LDS(DZ + i) = LDS(DZ + i) * scf;
+          }
+          for (int j = lane; j < n; j += 64) LDS(RD + j) = LDS(RD + j) * scf;
+          for (int i = lane; i < m; i += 64) LDS(RP + i) = LDS(RP + i) * scf;
+          SYNC();
+          ret = MP_POST_A + 100;  // marks the combined pass
+          next = MP_S0;
+          break;
         }
-        SYNC();
-        phase = P_ITER;
-        continue;
+        default:
+          done = true;
+          break;
       }
-      vop(VOP_PAIR, RZ, RS, T1, T2);           // kt3 = W rz, kt2 = W^-1 rs
-      const VopResult sr = vop(VOP_STEP, T1, T2, 0, 0);
-      if (sr.dom) {
-        status = ST_DOMAIN;
-        break;
+      if (done) break;
+      if (op >= 0) {
+        vr = vop(op, va, vb, vo1, vo2);
+        STAMP(SP_VOP);
       }
-      const double t = sr.r0;
-      if (phase == P_AFFINE) {
-        double kk = 0.0, ll = 0.0;
-        for (int i = lane; i < k; i += 64) {
-          kk += LDS(T2 + i) * LDS(T1 + i);
-          ll += LDS(LAM + i) * LDS(LAM + i);
-        }
-        kk = wsum(kk);
-        ll = wsum(ll);
-        const double rho = 1.0 - t - t * t * kk / ll;
-        const double cr = isnan(rho) ? rho : (rho < 0.0 ? 0.0 : (rho > 1.0 ? 1.0 : rho));
-        sig = (a.sigma_exp == 3) ? cr * cr * cr : pow(cr, (double)a.sigma_exp);
-        mu_ipm = ll / a.deg;
-        const double scf = 1.0 - sig;
-        vop(VOP_VPROD, T2, T1, K0, 0);         // kt1 = kt2 o kt3
-        for (int i = lane; i < k; i += 64) {
-          const double kt2 = sig * mu_ipm * e_of(i);
-          LDS(DS + i) = LDS(DS + i) + (kt2 - LDS(K0 + i));
-          LDS(DZ + i) = LDS(DZ + i) * scf;
-        }
-        for (int j = lane; j < n; j += 64) LDS(RD + j) = LDS(RD + j) * scf;
-        for (int i = lane; i < m; i += 64) LDS(RP + i) = LDS(RP + i) * scf;
-        SYNC();
-        phase = P_COMBINED;
-        continue;
-      }
-      // P_COMBINED: step and update (solver.jl:143-150)
-      const double stp = t * a.step;
-      for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(X_ + j) + LDS(RX + j) * stp;
-      for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(Y_ + i) + LDS(RY + i) * stp;
-      for (int i = lane; i < k; i += 64) {
-        LDS(Z_ + i) = LDS(Z_ + i) + LDS(RZ + i) * stp;
-        LDS(S_ + i) = LDS(S_ + i) + LDS(RS + i) * stp;
-      }
-      SYNC();
-      iters = ++it;
-      phase = P_ITER;
+      // the combined-pass marker routes the end of the second solve to MP_POST_A
+      phase = (next == MP_POST_A + 100) ? MP_POST_A : next;
     }
     if (a.mode == MODE_KKT) {
       if (lane == 0) a.status[p] = status;
       SYNC();
+      STAMP(SP_STORE);
       return;
     }
     for (int j = lane; j < n; j += 64) a.x[p * n + j] = LDS(X_ + j);
@@ -1207,6 +1468,14 @@ struct Small {
       a.status[p] = status;
     }
     SYNC();
+    STAMP(SP_STORE);
+#ifdef SOCP_STAMPS
+    if (lane == 0 && a.stamps) {
+      for (int i = 0; i < NSTAMP; ++i) atomicAdd(a.stamps + i, (unsigned long long)st_acc[i]);
+      atomicAdd(a.stamps + NSTAMP, (unsigned long long)iters);
+    }
+    for (int i = 0; i < NSTAMP; ++i) st_acc[i] = 0;
+#endif
   }
 };
 
@@ -1214,6 +1483,7 @@ template <int NQ, int NP, int MQ>
 __global__ void __launch_bounds__(64, 1) socp_small_kernel(SmallArgs args) {
   Small<NQ, NP, MQ> S(args);
   S.init_tables();
+  STAMP_START_S(S);
   while (true) {
     int p = 0;
     if (threadIdx.x == 0) p = atomicAdd(args.counter, 1);

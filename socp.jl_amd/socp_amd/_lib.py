@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # socp.jl_amd/
-LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libsocp.so")
+LIB_PATH = os.environ.get("SOCP_AMD_LIB") or os.path.join(_PKG_ROOT, "lib", "libsocp.so")
 HEADER = os.path.join(os.path.dirname(_PKG_ROOT), "include", "socp.h")
 
 # return codes / statuses / flags (include/socp.h)
@@ -25,6 +25,7 @@ EXPORTED = [
     "socp_ctx_destroy", "socp_ctx_sync", "socp_ctx_stream", "socp_supported",
     "socp_batch_solve", "socp_batch_solve_ex", "socp_batch_kkt_solve", "socp_generate",
     "socp_last_kernel_ms", "socp_last_kernel_name", "socp_debug_set_kkt_dump",
+    "socp_debug_set_stamps",
 ]
 
 
@@ -83,6 +84,7 @@ def load():
     L.socp_last_kernel_name.argtypes = [vp]
     L.socp_last_kernel_name.restype = C.c_char_p
     L.socp_debug_set_kkt_dump.argtypes = [vp]
+    L.socp_debug_set_stamps.argtypes = [vp]
     _lib = L
     return L
 

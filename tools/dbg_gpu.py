@@ -11,7 +11,7 @@ d = O.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
 n, m, k = cfg.n, cfg.m, cfg.k; cones = list(cfg.cones)
 A = d["A"].reshape(B, m*n)[0].reshape(n, m).T; G = d["G"].reshape(B, k*n)[0].reshape(n, k).T
 tr = O.solve_trace(cones, d["c"].reshape(B, n)[0], A, d["b"].reshape(B, m)[0], G, d["h"].reshape(B, k)[0], params=O.Params(maxit=12, tol=0.0), max_trace=13)
-buf = torch.zeros(2*n*n + 2*k, dtype=torch.float64, device="cuda")
+buf = torch.zeros(2*n*n + 2*k + n*m + m*m, dtype=torch.float64, device="cuda")
 S.default_context()
 _lib.load().socp_debug_set_kkt_dump(_lib.ptr(buf))
 rng = np.random.default_rng(0)

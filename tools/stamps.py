@@ -1,0 +1,29 @@
+"""Phase breakdown (shader-clock cycles per problem-iteration per wave) from the
+diagnostic build libsocp_stamps.so (SOCP_STAMPS).  Diagnostic only: its run time
+is not a benchmark number (stamps serialise the waits)."""
+import os, sys, time
+HERE = os.path.dirname(os.path.abspath(__file__))
+os.environ["SOCP_AMD_LIB"] = os.path.join(HERE, "..", "socp.jl_amd", "lib", "libsocp_stamps.so")
+sys.path.insert(0, os.path.join(HERE, "..", "socp.jl_amd"))
+import torch
+import socp_amd as S
+from socp_amd import _lib
+from socp_amd.configs import CONFIGS
+names = ["load", "scaling", "resid", "U", "SYRK", "sweepH", "schur", "solve", "step", "init", "store", "other"]
+for cname, B, K in (("C2", 8192, 8), ("C1", 4096, 3)):
+    cfg = CONFIGS[cname]
+    ctx = S.default_context()
+    c, A, b, G, h = S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    sing = torch.zeros(B, dtype=torch.uint8, device="cuda")
+    buf = torch.zeros(13, dtype=torch.int64, device="cuda")
+    _lib.load().socp_debug_set_stamps(_lib.ptr(buf))
+    out = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=K, tol=0.0)
+    ctx.sync(); buf.zero_()
+    out = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=K, tol=0.0)
+    ctx.sync()
+    v = buf.cpu().numpy().astype(float)
+    iters = v[12]
+    tot = v[:12].sum()
+    print(f"== {cname} B={B} K={K} kernel {ctx.last_kernel_ms():.2f} ms, iters {iters:.0f}, cycles/problem-iter {tot/iters:.0f}")
+    for nm, x in zip(names, v[:12]):
+        print(f"   {nm:8s} {x/iters:9.0f} cyc/it  {100*x/tot:5.1f}%")
