@@ -62,8 +62,8 @@ struct socp_ctx {
 };
 
 extern "C" const char* socp_last_error(void) { return g_err.c_str(); }
-#ifdef SOCP_STAMPS
-extern "C" const char* socp_version(void) { return "socp-mi355x 0.1 (gfx950, phase-stamp diagnostic build)"; }
+#ifdef SOCP_DIAG
+extern "C" const char* socp_version(void) { return "socp-mi355x 0.1 (gfx950, diagnostic build: phase stamps, KKT dumps)"; }
 #else
 extern "C" const char* socp_version(void) { return "socp-mi355x 0.1 (gfx950)"; }
 #endif
@@ -178,7 +178,7 @@ extern "C" int socp_supported(const socp_dims* d) {
 }
 
 // ---------------------------------------------------------------- launch
-static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_STAMPS builds)
+static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_DIAG builds)
 
 static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
   size_t lds = small_lds_bytes(v->NQ, v->NP, v->MQ);
@@ -327,13 +327,23 @@ extern "C" int socp_batch_solve(socp_ctx* ctx, const socp_dims* dims, const int3
 
 static double* g_kkt_debug = nullptr;  // device buffer for socp_debug_kkt (testing hook)
 extern "C" int socp_debug_set_stamps(unsigned long long* dev_buf) {
+#ifdef SOCP_DIAG
   g_stamps = dev_buf;
   return 0;
+#else
+  (void)dev_buf;
+  return fail(SOCP_E_UNSUPPORTED, "phase stamps exist only in the diagnostic build (libsocp_diag.so)");
+#endif
 }
 
 extern "C" int socp_debug_set_kkt_dump(double* dev_buf) {
+#ifdef SOCP_DIAG
   g_kkt_debug = dev_buf;
   return 0;
+#else
+  (void)dev_buf;
+  return fail(SOCP_E_UNSUPPORTED, "KKT dumps exist only in the diagnostic build (libsocp_diag.so)");
+#endif
 }
 
 extern "C" int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,

@@ -63,7 +63,7 @@ struct SmallArgs {
   double *cx, *cy, *cz, *cs;
   int32_t* counter;
   double* dbg;                 // optional (KKT mode): per problem H[n*n], Li[n*n], lam[k], wb[k]
-  unsigned long long* stamps;  // SOCP_STAMPS builds: per-phase cycle totals
+  unsigned long long* stamps;  // SOCP_DIAG builds: per-phase cycle totals
   ConeTable cones;
 };
 
@@ -110,9 +110,9 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
   return (size_t)total * sizeof(double);
 }
 
-// Diagnostic phase timing (separate build, -DSOCP_STAMPS): per-phase s_memtime
+// Diagnostic phase timing (separate build, -DSOCP_DIAG): per-phase s_memtime
 // deltas accumulated per problem and added to a global table by lane 0.
-#ifdef SOCP_STAMPS
+#ifdef SOCP_DIAG
 #define NSTAMP 12
 #define STAMP_DECL uint64_t st_last = 0; uint64_t st_acc[NSTAMP] = {0};
 #define STAMP_START_S(obj) do { __builtin_amdgcn_s_waitcnt(0); (obj).st_last = __builtin_amdgcn_s_memtime(); } while (0)
@@ -157,6 +157,11 @@ __device__ __forceinline__ double a_get_mfma(const AD& r) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// Scheduling fence: keeps the scheduler from hoisting the next unrolled step's
+// loads above this point (with H pinned in VGPRs and G in AGPRs, hoisting
+// across steps is what overflows the register file).
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -181,6 +186,30 @@ __device__ __forceinline__ double dpp(double v) {
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// Lane ids re-read inside each phase (LANE_IDS shadows the members): values
+// derived from them (4*pp + g, 16*ti + cl, ...) are then recomputed where they
+// are used instead of being hoisted out of the persistent loop and kept live.
+__device__ __forceinline__ int lane_fresh() {
+  int v = (int)threadIdx.x;
+  asm volatile("" : "+v"(v));
+  return v;
+}
+#define LANE_IDS()                      \
+  const int lane = lane_fresh();        \
+  const int g = lane >> 4, cl = lane & 15; \
+  (void)g; (void)cl
+
+// Wave-uniform copies.  LLVM's divergence analysis treats every LDS or global
+// load as divergent; a branch on such a value (the sweep's pivot test, the
+// per-problem `sing` flag, the phase number) is then compiled as exec-masked
+// straight-line code: every arm runs and the live ranges of all arms merge.
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double uni(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
   return __hiloint2double(hi, lo);
 }
 
@@ -319,7 +348,6 @@ struct Small {
 
   AD G[NP][NQ];  // AGPR-resident
   d4 T[NT];
-  AD AL[NQ * MQ][4];  // ALi' tiles, AGPR-resident
   d4 Sv[MT];
 
   __device__ __forceinline__ Small(const SmallArgs& args)
@@ -366,14 +394,20 @@ struct Small {
   }
 
   __device__ __forceinline__ void load_problem(int64_t p) {
+    LANE_IDS();
     const double* Gp = a.G + p * (int64_t)k * n;
+    // padding (row >= k or col >= n) reads element 0 and is zeroed with an
+    // integer mask: no per-element exec mask is materialised
 #pragma unroll
     for (int pp = 0; pp < NP; ++pp) {
       const int row = 4 * pp + g;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const int col = 16 * q + cl;
-        a_put(G[pp][q], (row < k && col < n) ? Gp[(int64_t)col * k + row] : 0.0);
+        const int ok = (row < k) & (col < n);
+        const int64_t idx = ok ? (int64_t)col * k + row : 0;
+        const uint64_t bits = (uint64_t)__double_as_longlong(Gp[idx]) & (0ull - (uint64_t)ok);
+        a_put(G[pp][q], __longlong_as_double((long long)bits));
       }
     }
     for (int e = lane; e < 16 * KMAX; e += 64) LDS(O_KV + e) = 0.0;
@@ -419,6 +453,7 @@ struct Small {
   // in two rounds STEP1/STEP2), max_step (mats.jl:1-28).  a, b, o1, o2 are
   // LDS offsets of k-vectors.  Exactly one instance (called from run()).
   __device__ __forceinline__ VopResult vop(int op, int a_, int b_, int o1, int o2) {
+    LANE_IDS();
     double v[2][3];
     bool mxp = false;
     int nvals = 1;
@@ -679,9 +714,10 @@ struct Small {
 
   // U[c,:] = (sum_{i in cone c} w_i G[i,:]) / (1+wb0), w_head = -(1+wb0), w_tail = wb_i
   __device__ __forceinline__ void compute_U() {
+    LANE_IDS();
     for (int c = 0; c < nc; ++c) {
-      if ((int)LDS(O_CKIND + c) != SOC_K) continue;
-      const int o = (int)LDS(O_COFF + c), d = (int)LDS(O_CDIM + c);
+      if (uni((int)LDS(O_CKIND + c)) != SOC_K) continue;
+      const int o = uni((int)LDS(O_COFF + c)), d = uni((int)LDS(O_CDIM + c));
       const double wb0 = LDS(WB + o);
       double acc[NQ];
 #pragma unroll
@@ -712,6 +748,7 @@ struct Small {
 
   // ----------------------------------------------------- H = X'X (+A'A)
   __device__ __forceinline__ void form_H(bool addAA) {
+    LANE_IDS();
 #pragma unroll
     for (int t = 0; t < NT; ++t) T[t] = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -727,6 +764,7 @@ struct Small {
       for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
         for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = mfma(X[ti], X[tj], T[tri(ti, tj)]);
+      if (pp % 2 == 1) SCHED_FENCE();
     }
     if (addAA) {
 #pragma unroll
@@ -758,6 +796,7 @@ struct Small {
   // one LAPACK potrf applies inside cholesky! (ajj <= 0 or NaN).
   template <int Q>
   __device__ __forceinline__ bool sweep(d4 (&M)[Q * (Q + 1) / 2], int nact) {
+    LANE_IDS();
     for (int p = 0; p < nact; ++p) {
       const int cb = O_COL + (p & 1) * SH::CB;
       const int tp = p >> 4, pc = p & 15, pr = pc >> 2, pg = pc & 3;
@@ -772,12 +811,16 @@ struct Small {
           if (ti == tp && tj < tp && g == pg) LDS(cb + 16 * tj + cl) = sel4(M[tri(ti, tj)], pr);
         }
       SYNC();
-      const double d = LDS(cb + p);
+      const double d = uni(LDS(cb + p));
       if (!(d > 0.0)) return false;
       const double rinv = recip(d);
       double cC[Q];
 #pragma unroll
       for (int ti = 0; ti < Q; ++ti) cC[ti] = LDS(cb + 16 * ti + cl) * rinv;
+      // row p of tile row tp sits in lanes g == pg, entry pr; column p of
+      // tile column tp in lanes cl == pc (ti, tj, r compile-time; tp, pr
+      // uniform: no per-lane row/column index is kept live)
+      const bool lane_c = cl == pc, lane_r = g == pg;
 #pragma unroll
       for (int ti = 0; ti < Q; ++ti) {
         double cR[4];
@@ -787,10 +830,10 @@ struct Small {
         for (int tj = 0; tj <= ti; ++tj) {
           d4& t = M[tri(ti, tj)];
           if (ti == tp || tj == tp) {
+            const bool iC = (tj == tp) && lane_c;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const int R = 16 * ti + g + 4 * r, Cc = 16 * tj + cl;
-              const bool iR = R == p, iC = Cc == p;
+              const bool iR = (ti == tp) && (pr == r) && lane_r;
               const double gen = fma(-cR[r], cC[tj], t[r]);
               // pivot row and column both come from the gathered column p:
               // re-symmetrising them every step is what keeps the sweep's
@@ -809,6 +852,7 @@ struct Small {
   }
 
   __device__ __forceinline__ d4 transpose(d4 t) {
+    LANE_IDS();
     SYNC();
 #pragma unroll
     for (int r = 0; r < 4; ++r) LDS(O_TB + (g + 4 * r) * 17 + cl) = t[r];
@@ -836,20 +880,24 @@ struct Small {
 
   // H (+A'A) -> sweep -> Li;  ALi' = Li A' (n x m);  S = A ALi';  S^-1.
   __device__ __forceinline__ int factor(bool identity, bool addAA) {
+    LANE_IDS();
     STAMP(SP_OTHER);
     if (!identity) compute_U();
     STAMP(SP_U);
     form_H(addAA);
     SYNC();
     STAMP(SP_SYRK);
-    // debug dump per problem: H, -H^-1 (n x n each), lam, wbar (k each), ALi' (n x m), S (m x m)
+#ifdef SOCP_DIAG
+    // diagnostic dump per problem: H, H^-1 (n x n each), lam, wbar (k each), Li A' (n x m), S (m x m)
     double* dbg = (a.dbg && a.mode == MODE_KKT) ? a.dbg + dbg_p * (int64_t)(2 * n * n + 2 * k + n * m + m * m) : nullptr;
     if (dbg) dump_sym(dbg);
+#endif
     const bool okH = sweep<NQ>(T, n);
     STAMP(SP_SWEEP_H);
     if (!okH) return ST_CHOL_H;
 #pragma unroll
     for (int t = 0; t < NT; ++t) T[t] = -T[t];
+#ifdef SOCP_DIAG
     if (dbg) {
       dump_sym(dbg + n * n);
       for (int i = lane; i < k; i += 64) {
@@ -857,41 +905,49 @@ struct Small {
         dbg[2 * n * n + k + i] = LDS(WB + i);
       }
     }
+#endif
+    // S = A Li A' (densesolver.jl:49-50: ALi = A*Li, S = ALi*A'), one 16-column
+    // tile of Li A' at a time: it lives only here, the solves use A (Li n0).
 #pragma unroll
-    for (int ti = 0; ti < NQ; ++ti) {
-      d4 acc[MQ];
+    for (int tq = 0; tq < MQ; ++tq) {
+      d4 ALc[NQ];
 #pragma unroll
-      for (int tm = 0; tm < MQ; ++tm) acc[tm] = (d4){0.0, 0.0, 0.0, 0.0};
+      for (int ti = 0; ti < NQ; ++ti) {
+        d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int tk = 0; tk < NQ; ++tk) {
-        d4 Ut;
-        if (tk >= ti)
-          Ut = T[tri(tk, ti)];
-        else
-          Ut = transpose(T[tri(ti, tk)]);
+        for (int tk = 0; tk < NQ; ++tk) {
+          d4 Ut;
+          if (tk >= ti)
+            Ut = T[tri(tk, ti)];
+          else
+            Ut = transpose(T[tri(ti, tk)]);
 #pragma unroll
-        for (int tm = 0; tm < MQ; ++tm)
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-            acc[tm] = mfma(Ut[s], LDS(O_A + (16 * tm + cl) * LDA + 16 * tk + g + 4 * s), acc[tm]);
+          for (int s = 0; s < 4; ++s) acc = mfma(Ut[s], LDS(O_A + (16 * tq + cl) * LDA + 16 * tk + g + 4 * s), acc);
+        }
+        ALc[ti] = acc;
       }
+#ifdef SOCP_DIAG
+      if (dbg) {
+        double* dA = dbg + 2 * n * n + 2 * k;
 #pragma unroll
-      for (int tm = 0; tm < MQ; ++tm)
+        for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) a_put(AL[ti * MQ + tm][r], acc[tm][r]);
-    }
+          for (int r = 0; r < 4; ++r) {
+            const int R = 16 * ti + g + 4 * r, Cc = 16 * tq + cl;
+            if (R < n && Cc < m) dA[R * m + Cc] = ALc[ti][r];
+          }
+      }
+#endif
 #pragma unroll
-    for (int tm = 0; tm < MQ; ++tm)
-#pragma unroll
-      for (int tq = 0; tq <= tm; ++tq) {
+      for (int tm = tq; tm < MQ; ++tm) {
         d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int tk = 0; tk < NQ; ++tk)
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
-            acc = mfma(LDS(O_A + (16 * tm + cl) * LDA + 16 * tk + g + 4 * s), a_get_mfma(AL[tk * MQ + tq][s]), acc);
+          for (int s = 0; s < 4; ++s) acc = mfma(LDS(O_A + (16 * tm + cl) * LDA + 16 * tk + g + 4 * s), ALc[tk][s], acc);
         Sv[tri(tm, tq)] = acc;
       }
+    }
 #pragma unroll
     for (int tm = 0; tm < MQ; ++tm)
 #pragma unroll
@@ -899,19 +955,9 @@ struct Small {
         const int R = 16 * tm + g + 4 * r, Cc = 16 * tm + cl;
         if (R == Cc && R >= m) Sv[tri(tm, tm)][r] = 1.0;
       }
+#ifdef SOCP_DIAG
     if (dbg) {
-      double* dA = dbg + 2 * n * n + 2 * k;
-      double* dS = dA + n * m;
-#pragma unroll
-      for (int ti = 0; ti < NQ; ++ti)
-#pragma unroll
-        for (int tm = 0; tm < MQ; ++tm)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int R = 16 * ti + g + 4 * r, Cc = 16 * tm + cl;
-            const double v = a_get(AL[ti * MQ + tm][r]);
-            if (R < n && Cc < m) dA[R * m + Cc] = v;
-          }
+      double* dS = dbg + 2 * n * n + 2 * k + n * m;
 #pragma unroll
       for (int tm = 0; tm < MQ; ++tm)
 #pragma unroll
@@ -922,6 +968,7 @@ struct Small {
             if (R < m && Cc < m) dS[R * m + Cc] = Sv[tri(tm, tq)][r];
           }
     }
+#endif
     SYNC();
     const bool okS = sweep<MQ>(Sv, m);
     STAMP(SP_SCHUR);
@@ -936,6 +983,7 @@ struct Small {
   // part (transposed off-diagonal tiles): reduce over the 4 row groups.
   template <int Q>
   __device__ __forceinline__ void symv(const d4 (&M)[Q * (Q + 1) / 2], int vin, int vout) {
+    LANE_IDS();
     double vc[Q], P2[Q];
 #pragma unroll
     for (int t = 0; t < Q; ++t) {
@@ -988,6 +1036,7 @@ struct Small {
   // Rows are reduced over the 16 column lanes in chunks of up to 8 row-steps.
   template <int P0, int CH>
   __device__ __forceinline__ void gemv_G_chunk(const double (&uq)[NQ], int add1, int add2, int out) {
+    LANE_IDS();
     double P[CH];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
@@ -1015,6 +1064,7 @@ struct Small {
     }
   }
   __device__ __forceinline__ void gemv_G(int u, int add1, int add2, int out) {
+    LANE_IDS();
     double uq[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) uq[q] = LDS(u + 16 * q + cl);
@@ -1024,6 +1074,7 @@ struct Small {
 
   // acc[q] (all lanes) = (G' v)[16q+cl]
   __device__ __forceinline__ void gemv_Gt(int v, double (&acc)[NQ]) {
+    LANE_IDS();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
 #pragma unroll
@@ -1039,37 +1090,65 @@ struct Small {
     }
   }
 
-  __device__ __forceinline__ double At_times(int v, int j) {
-    double acc = 0.0;
-    for (int r = 0; r < m; ++r) acc = fma(LDS(O_A + r * LDA + j), LDS(v + r), acc);
-    return acc;
+  // acc[q] (all lanes) = (A' v)[16q+cl]: rows split over the 4 lane groups
+  __device__ __forceinline__ void At_mv(int v, double (&acc)[NQ]) {
+    LANE_IDS();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+#pragma unroll
+    for (int s = 0; s < MQ * 4; ++s) {
+      const int i = g + 4 * s;
+      const double vi = LDS(v + i);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[q] = fma(LDS(O_A + i * LDA + 16 * q + cl), vi, acc[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      acc[q] += __shfl_xor(acc[q], 16);
+      acc[q] += __shfl_xor(acc[q], 32);
+    }
   }
-  __device__ __forceinline__ double A_times(int v, int i) {
-    double acc = 0.0;
-    for (int j = 0; j < n; ++j) acc = fma(LDS(O_A + i * LDA + j), LDS(v + j), acc);
-    return acc;
+  // out[i] = (A u)[i] - sub[i] for i < m (columns split over the 4 lane groups);
+  // returns sum of out[i]^2 on lanes g == 0
+  __device__ __forceinline__ double A_mv(int u, int sub, int out) {
+    LANE_IDS();
+    double sq = 0.0;
+#pragma unroll
+    for (int tm = 0; tm < MQ; ++tm) {
+      const int i = 16 * tm + cl;
+      double acc = 0.0;
+#pragma unroll
+      for (int t = 0; t < NQ * 4; ++t) acc = fma(LDS(O_A + i * LDA + g + 4 * t), LDS(u + g + 4 * t), acc);
+      acc += __shfl_xor(acc, 16);
+      acc += __shfl_xor(acc, 32);
+      if (g == 0 && i < m) {
+        const double v = acc - LDS(sub + i);
+        LDS(out + i) = v;
+        sq = fma(v, v, sq);
+      }
+    }
+    return sq;
   }
 
   // rd = A'y + G'z + c, rp = Ax - b, rz = Gx + s - h (solver.jl:109-118)
   __device__ __forceinline__ void residuals(double& nd, double& np_, double& gap) {
-    double acc[NQ];
+    LANE_IDS();
+    double acc[NQ], at[NQ];
     gemv_Gt(Z_, acc);
+    At_mv(Y_, at);
+    double d2 = 0.0, zs = 0.0;
     if (g == 0) {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) LDS(TN + 16 * q + cl) = acc[q];
+      for (int q = 0; q < NQ; ++q) {
+        const int j = 16 * q + cl;
+        if (j < n) {
+          const double v = (at[q] + acc[q]) + LDS(C_ + j);
+          LDS(RD + j) = v;
+          d2 = fma(v, v, d2);
+        }
+      }
     }
-    SYNC();
-    double d2 = 0.0, p2 = 0.0, zs = 0.0;
-    if (lane < n) {
-      const double v = At_times(Y_, lane) + LDS(TN + lane) + LDS(C_ + lane);
-      LDS(RD + lane) = v;
-      d2 = v * v;
-    }
-    if (lane < m) {
-      const double v = A_times(X_, lane) - LDS(B_ + lane);
-      LDS(RP + lane) = v;
-      p2 = v * v;
-    }
+    const double p2 = A_mv(X_, B_, RP);
     gemv_G(X_, S_, H_, DZ);
     for (int i = lane; i < k; i += 64) zs += LDS(Z_ + i) * LDS(S_ + i);
     nd = sqrt(wsum(d2));
@@ -1078,49 +1157,42 @@ struct Small {
   }
 
   // The matrix part of solve_kkt(::DenseSolver) (densesolver.jl:66-85), between
-  // the cone ops: n0 = GWiWi*k2 + dx (+A'dy if sing); m0 = ALi*n0 - dy;
-  // cy = S^-1 m0; m0 = sing ? dy - cy : -cy (init: -cy); n0 += A'm0;
-  // cx = Li n0; k1 = G cx - k2.   In: RD RP T2(=W^-2 k2) K2.  Out: RX RY K1.
+  // the cone ops: n0 = GWiWi*k2 + dx (+A'dy if sing); m0 = ALi*n0 - dy, taken as
+  // A*(Li*n0) - dy; cy = S^-1 m0; m0 = sing ? dy - cy : -cy (init: -cy);
+  // n0 += A'm0; cx = Li n0; k1 = G cx - k2.   In: RD RP T2(=W^-2 k2) K2.  Out: RX RY K1.
   __device__ __forceinline__ void solve_matrix_part(bool init) {
-    double acc[NQ];
-    gemv_Gt(T2, acc);
-    if (g == 0) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) LDS(TN + 16 * q + cl) = acc[q];
-    }
-    SYNC();
-    if (lane < n) {
-      double v = LDS(TN + lane) + LDS(RD + lane);
-      if (sing) v = v + At_times(RP, lane);
-      LDS(N0 + lane) = v;
-    }
-    SYNC();
+    LANE_IDS();
     {
-      double vr[NQ][4];
+      double acc[NQ], at[NQ];
+      gemv_Gt(T2, acc);
+      if (sing) At_mv(RP, at);
+      if (g == 0) {
 #pragma unroll
-      for (int t = 0; t < NQ; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) vr[t][r] = LDS(N0 + 16 * t + g + 4 * r);
-#pragma unroll
-      for (int tm = 0; tm < MQ; ++tm) {
-        double pacc = 0.0;
-#pragma unroll
-        for (int ti = 0; ti < NQ; ++ti)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pacc = fma(a_get(AL[ti * MQ + tm][r]), vr[ti][r], pacc);
-        pacc += __shfl_xor(pacc, 16);
-        pacc += __shfl_xor(pacc, 32);
-        const int i = 16 * tm + cl;
-        if (g == 0 && i < m) LDS(M0 + i) = pacc - LDS(RP + i);
+        for (int q = 0; q < NQ; ++q) {
+          const int j = 16 * q + cl;
+          double v = acc[q] + LDS(RD + j);
+          if (sing) v = v + at[q];
+          LDS(N0 + j) = v;
+        }
       }
     }
     SYNC();
-    symv<MQ>(Sv, M0, RY);
+    symv<NQ>(T, N0, TN);   // Li n0
+    A_mv(TN, RP, M0);      // m0 = A Li n0 - dy
+    SYNC();
+    symv<MQ>(Sv, M0, RY);  // cy = S^-1 m0
     if (lane < m) LDS(M0 + lane) = (sing && !init) ? LDS(RP + lane) - LDS(RY + lane) : -LDS(RY + lane);
     SYNC();
-    if (lane < n) LDS(N0 + lane) = LDS(N0 + lane) + At_times(M0, lane);
+    {
+      double at[NQ];
+      At_mv(M0, at);
+      if (g == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) LDS(N0 + 16 * q + cl) = LDS(N0 + 16 * q + cl) + at[q];
+      }
+    }
     SYNC();
-    symv<NQ>(T, N0, RX);
+    symv<NQ>(T, N0, RX);   // cx = Li n0
     gemv_G(RX, -1, K2, K1);
   }
 
@@ -1161,7 +1233,7 @@ struct Small {
     SYNC();
     int phase;
     if (a.sing) {
-      sing = a.sing[p] != 0;
+      sing = uni((int)a.sing[p]) != 0;
       phase = after_singtest;
     } else {
       sing = false;
@@ -1169,6 +1241,7 @@ struct Small {
     }
     bool done = false;
     while (!done) {
+      LANE_IDS();
       int op = -1, va = 0, vb = 0, vo1 = 0, vo2 = 0;
       int next = phase;
       switch (phase) {
@@ -1439,12 +1512,13 @@ struct Small {
           break;
       }
       if (done) break;
+      op = uni(op);
       if (op >= 0) {
-        vr = vop(op, va, vb, vo1, vo2);
+        vr = vop(op, uni(va), uni(vb), uni(vo1), uni(vo2));
         STAMP(SP_VOP);
       }
       // the combined-pass marker routes the end of the second solve to MP_POST_A
-      phase = (next == MP_POST_A + 100) ? MP_POST_A : next;
+      phase = uni((next == MP_POST_A + 100) ? MP_POST_A : next);
     }
     if (a.mode == MODE_KKT) {
       if (lane == 0) a.status[p] = status;
@@ -1469,7 +1543,7 @@ struct Small {
     }
     SYNC();
     STAMP(SP_STORE);
-#ifdef SOCP_STAMPS
+#ifdef SOCP_DIAG
     if (lane == 0 && a.stamps) {
       for (int i = 0; i < NSTAMP; ++i) atomicAdd(a.stamps + i, (unsigned long long)st_acc[i]);
       atomicAdd(a.stamps + NSTAMP, (unsigned long long)iters);

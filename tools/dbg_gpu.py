@@ -1,4 +1,5 @@
 import sys, os
+os.environ["SOCP_AMD_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "socp.jl_amd", "lib", "libsocp_diag.so")
 import numpy as np, torch
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "socp.jl_amd"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))

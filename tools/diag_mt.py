@@ -2,6 +2,7 @@
 hook) for C1/C2-shaped problems and reports the error per 16x16 tile against
 numpy, plus the KKT solution against the oracle."""
 import sys, os
+os.environ["SOCP_AMD_LIB"] = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "socp.jl_amd", "lib", "libsocp_diag.so")
 import numpy as np, torch
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "socp.jl_amd"))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))

@@ -1,15 +1,15 @@
 """Phase breakdown (shader-clock cycles per problem-iteration per wave) from the
-diagnostic build libsocp_stamps.so (SOCP_STAMPS).  Diagnostic only: its run time
+diagnostic build libsocp_diag.so (SOCP_STAMPS).  Diagnostic only: its run time
 is not a benchmark number (stamps serialise the waits)."""
 import os, sys, time
 HERE = os.path.dirname(os.path.abspath(__file__))
-os.environ["SOCP_AMD_LIB"] = os.path.join(HERE, "..", "socp.jl_amd", "lib", "libsocp_stamps.so")
+os.environ["SOCP_AMD_LIB"] = os.path.join(HERE, "..", "socp.jl_amd", "lib", "libsocp_diag.so")
 sys.path.insert(0, os.path.join(HERE, "..", "socp.jl_amd"))
 import torch
 import socp_amd as S
 from socp_amd import _lib
 from socp_amd.configs import CONFIGS
-names = ["load", "scaling", "resid", "U", "SYRK", "sweepH", "schur", "solve", "step", "init", "store", "other"]
+names = ["load", "scaling", "resid", "U", "SYRK", "sweepH", "schur", "solve", "step", "vop", "store", "other"]
 for cname, B, K in (("C2", 8192, 8), ("C1", 4096, 3)):
     cfg = CONFIGS[cname]
     ctx = S.default_context()
