@@ -90,7 +90,9 @@ __host__ __device__ constexpr int kv(int id) { return O_KV + id * KMAX; }
 template <int NQ, int NP, int MQ>
 struct Shape {
   static constexpr int NPAD = 16 * NQ, KP = 4 * NP, MPAD = 16 * MQ, LDA = NPAD + 1;
-  static constexpr int CB = (NPAD > MPAD ? NPAD : MPAD);
+  // sweep gather buffer: pivot column of the diagonal tile [16] + pivot row of
+  // every tile of the panel slab [16 per tile]
+  static constexpr int CB = 16 + (NPAD > MPAD ? NPAD : MPAD);
   static constexpr int O_A = O_FIXED_END;
   static constexpr int O_NV = O_A + MPAD * LDA;    // n-vectors: c x rd rx n0 tn
   static constexpr int O_MV = O_NV + 6 * NPAD;     // m-vectors: b y rp ry m0 tm
@@ -105,7 +107,7 @@ enum : int { NV_C, NV_X, NV_RD, NV_RX, NV_N0, NV_TN };
 enum : int { MV_B, MV_Y, MV_RP, MV_RY, MV_M0, MV_TM };
 
 inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
-  int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = NPAD + 1, CB = NPAD > MPAD ? NPAD : MPAD;
+  int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = NPAD + 1, CB = 16 + (NPAD > MPAD ? NPAD : MPAD);
   int total = O_FIXED_END + MPAD * LDA + 6 * NPAD + 6 * MPAD + NCS * NPAD + 2 * CB + 16 * 17;
   return (size_t)total * sizeof(double);
 }
@@ -794,58 +796,105 @@ struct Small {
   // matrix held as lower tiles in C/D layout; leaves -M^-1 there.  Pivot p is
   // the Schur complement = (Cholesky diagonal)^2, so the failure test is the
   // one LAPACK potrf applies inside cholesky! (ajj <= 0 or NaN).
+  //
+  // Blocked by 16-pivot panels P.  The 16 single-pivot steps run only on the
+  // panel slab [M_PP | Z] (Z_i = M_Pi, rows P, cols i != P), which they turn
+  // into [-M_PP^-1 | M_PP^-1 Z].  The rank-1 updates the single-pivot sweep
+  // would apply to every other tile are deferred: at step c the current row c
+  // of Z over sqrt(d_c) is row c of W = L_PP^-1 Z, and M_OO -= W'W is applied
+  // once per panel with MFMA -- the same sum of rank-1 terms (Gram form, as
+  // accurate as the unblocked sweep; the explicit -M_PP^-1-based update is not).
   template <int Q>
   __device__ __forceinline__ bool sweep(d4 (&M)[Q * (Q + 1) / 2], int nact) {
     LANE_IDS();
-    for (int p = 0; p < nact; ++p) {
-      const int cb = O_COL + (p & 1) * SH::CB;
-      const int tp = p >> 4, pc = p & 15, pr = pc >> 2, pg = pc & 3;
+    int step = 0;
 #pragma unroll
-      for (int ti = 0; ti < Q; ++ti)
+    for (int P = 0; P < Q; ++P) {
+      if (16 * P >= nact) break;
+      const int cnt = (nact - 16 * P) < 16 ? (nact - 16 * P) : 16;
+      d4 Z[Q], W[Q];
 #pragma unroll
-        for (int tj = 0; tj <= ti; ++tj) {
-          if (tj == tp && cl == pc) {
+      for (int i = 0; i < Q; ++i) {
+        W[i] = (d4){0.0, 0.0, 0.0, 0.0};
+        if (i < P) Z[i] = M[tri(P, i)];
+        if (i > P) Z[i] = transpose(M[tri(i, P)]);
+      }
+      d4& D = M[tri(P, P)];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) LDS(cb + 16 * ti + g + 4 * r) = M[tri(ti, tj)][r];
+      for (int pr = 0; pr < 4; ++pr) {
+        for (int pg = 0; pg < 4; ++pg) {
+          const int c = 4 * pr + pg;
+          if (c >= cnt) break;
+          const int cb = O_COL + (step & 1) * SH::CB;
+          ++step;
+          const bool lane_c = cl == c, lane_r = g == pg;
+          // gather: column c of the diagonal tile, row c of every slab tile
+          if (lane_c) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) LDS(cb + g + 4 * r) = D[r];
           }
-          if (ti == tp && tj < tp && g == pg) LDS(cb + 16 * tj + cl) = sel4(M[tri(ti, tj)], pr);
-        }
-      SYNC();
-      const double d = uni(LDS(cb + p));
-      if (!(d > 0.0)) return false;
-      const double rinv = recip(d);
-      double cC[Q];
+          if (lane_r) {
+            LDS(cb + 16 + 16 * P + cl) = D[pr];
 #pragma unroll
-      for (int ti = 0; ti < Q; ++ti) cC[ti] = LDS(cb + 16 * ti + cl) * rinv;
-      // row p of tile row tp sits in lanes g == pg, entry pr; column p of
-      // tile column tp in lanes cl == pc (ti, tj, r compile-time; tp, pr
-      // uniform: no per-lane row/column index is kept live)
-      const bool lane_c = cl == pc, lane_r = g == pg;
+            for (int i = 0; i < Q; ++i)
+              if (i != P) LDS(cb + 16 + 16 * i + cl) = Z[i][pr];
+          }
+          SYNC();
+          const double d = uni(LDS(cb + c));
+          if (!(d > 0.0)) return false;
+          const double rinv = recip(d);
+          const double isd = recip(sqrt(d));
+          double cR[4];
 #pragma unroll
-      for (int ti = 0; ti < Q; ++ti) {
-        double cR[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cR[r] = LDS(cb + 16 * ti + g + 4 * r);
-#pragma unroll
-        for (int tj = 0; tj <= ti; ++tj) {
-          d4& t = M[tri(ti, tj)];
-          if (ti == tp || tj == tp) {
-            const bool iC = (tj == tp) && lane_c;
+          for (int r = 0; r < 4; ++r) cR[r] = LDS(cb + g + 4 * r);
+          // diagonal tile: pivot row and column both from the gathered column
+          // (re-symmetrised every step, which keeps the inverse a good
+          // right-inverse at kappa ~ 1e10)
+          {
+            const double cC = LDS(cb + cl) * rinv;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const bool iR = (ti == tp) && (pr == r) && lane_r;
-              const double gen = fma(-cR[r], cC[tj], t[r]);
-              // pivot row and column both come from the gathered column p:
-              // re-symmetrising them every step is what keeps the sweep's
-              // inverse a good right-inverse at kappa ~ 1e10.
+              const double gen = fma(-cR[r], cC, D[r]);
               const double scol = cR[r] * rinv;
-              t[r] = (iR && iC) ? -rinv : (iC ? scol : (iR ? cC[tj] : gen));
+              const bool iR = (r == pr) && lane_r;
+              D[r] = (iR && lane_c) ? -rinv : (lane_c ? scol : (iR ? cC : gen));
             }
-          } else {
+          }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) t[r] = fma(-cR[r], cC[tj], t[r]);
+          for (int i = 0; i < Q; ++i) {
+            if (i == P) continue;
+            const double rc = LDS(cb + 16 + 16 * i + cl);  // M[c][col]
+            const double rs = rc * rinv;
+            if (lane_r) W[i][pr] = rc * isd;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const double gen = fma(-cR[r], rs, Z[i][r]);
+              Z[i][r] = (r == pr && lane_r) ? rs : gen;
+            }
           }
         }
+      }
+      // M_OO -= W'W (lower tiles of every other block row/column)
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        if (i == P) continue;
+        d4 Wn;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Wn[r] = -W[i][r];
+#pragma unroll
+        for (int j = i; j < Q; ++j) {
+          if (j == P) continue;
+          // tile (j, i), j >= i: += W_j' (-W_i)
+          d4 acc = M[tri(j, i)];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc = mfma(W[j][s], Wn[s], acc);
+          M[tri(j, i)] = acc;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        if (i < P) M[tri(P, i)] = Z[i];
+        if (i > P) M[tri(i, P)] = transpose(Z[i]);
       }
     }
     return true;

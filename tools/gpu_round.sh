@@ -12,5 +12,5 @@ timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 || { tail -30 gpur
 tail -2 gpurun_out/bench.log
 timeout -k 10 300 python tools/stamps.py > gpurun_out/stamps.log 2>&1 || { tail -30 gpurun_out/stamps.log; exit 1; }
 cat gpurun_out/stamps.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o r01 -- python bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
-find gpurun_out/prof -name "*stats*" | head
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d gpurun_out/prof -o r01 -- python bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof.log 2>&1 || { tail -30 gpurun_out/prof.log; exit 1; }
+find gpurun_out/prof -name "*stats*"; python tools/rocpd_summary.py $(find gpurun_out/prof -name "*.db" | head -1) gpurun_out/kernel_stats.csv && head -3 gpurun_out/kernel_stats.csv
