@@ -74,14 +74,20 @@ enum : int {
   O_COFF = O_RC + KMAX,      // cone offs[NCS]
   O_CDIM = O_COFF + NCS,     // cone dim[NCS]
   O_CKIND = O_CDIM + NCS,    // cone kind[NCS]
-  O_MU = O_CKIND + NCS,      // mu per cone
-  O_I1 = O_MU + NCS,         // 1/(1+wb0) per cone
-  O_TOT = O_I1 + NCS,        // reduced values per cone [NCS][4]
-  O_PART = O_TOT + 4 * NCS,  // per-slot partials [2][NCS][4]
-  O_CST = O_PART + 8 * NCS,  // step-length scratch per cone [NCS][4]
-  O_KV = O_CST + 4 * NCS,    // 16 k-vectors of KMAX
+  O_CC = O_CKIND + NCS,        // per-cone constants of the current scaling [NCC][NCS]
+  O_PART = O_CC + 12 * NCS,    // segment partials [NVMAX][NCS][2 slots] (zero where unused)
+  O_TOTC = O_PART + 4 * NCS * 2,  // per-cone results [2][NCS]
+  O_KV = O_TOTC + 2 * NCS,     // 16 k-vectors of KMAX
   O_FIXED_END = O_KV + 16 * KMAX
 };
+// per-cone constants (SOC cones), recomputed by every scaling:
+//   MU = mu, IMU = 1/mu, WB0 = wbar_0, I1 = 1/(1+wbar_0), W2 = |wbar_1|^2,
+//   L0 = lambda_0, AA = lambda_0^2 - |lambda_1|^2 (iprod!'s `a`, vectors.jl:105),
+//   IAA = 1/AA, IL0 = 1/lambda_0, IL0AA = 1/(lambda_0 AA),
+//   SA = 1/sqrt(AA) (scmax's `a`, mats.jl:66), SAL = 1/(SA lambda_0 + 1)
+enum : int { CC_MU, CC_IMU, CC_WB0, CC_I1, CC_W2, CC_L0, CC_AA, CC_IAA, CC_IL0, CC_IL0AA, CC_SA,
+             CC_SAL };
+__host__ __device__ constexpr int cc(int q, int c) { return O_CC + q * NCS + c; }
 // k-vector ids
 enum : int { KV_H, KV_Z, KV_S, KV_DZ, KV_DS, KV_RZ, KV_RS, KV_LAM, KV_WB, KV_CA, KV_CB, KV_K0,
              KV_K1, KV_K2, KV_T1, KV_T2 };
@@ -129,7 +135,15 @@ enum { SP_LOAD, SP_SCALING, SP_RESID, SP_U, SP_SYRK, SP_SWEEP_H, SP_SCHUR, SP_SO
 
 extern __shared__ double socp_lds[];
 #define LDS(i) socp_lds[(i)]
-#define SYNC() __syncthreads()
+// Blocks are one wavefront: LDS instructions of a wave execute in issue order,
+// so an LDS hand-off between lanes needs only a wave-scope fence (no s_barrier,
+// no lgkmcnt drain) -- the rocPRIM wave_barrier() idiom.
+#define SYNC()                                             \
+  do {                                                     \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
+    __builtin_amdgcn_wave_barrier();                       \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
+  } while (0)
 
 // A double pinned in two AGPRs (gfx950: VALU cannot read AGPRs; MFMA can).
 // G lives here for the whole solve and is copied to VGPRs at each use.
@@ -304,22 +318,12 @@ struct RSCount<C, 0> {
   static constexpr int value = C;
 };
 
-// cone vector operations (one instance, Small::vop)
-enum : int { VOP_SCALE, VOP_ISCALE, VOP_PAIR, VOP_IPROD, VOP_VPROD, VOP_SCALING, VOP_STEP1,
-             VOP_STEP2, VOP_MAXSTEP };
-
-struct VopResult {
-  double r0, r1;
-  int dom;
-};
-
-// driver micro-phases
+// driver micro-phases and solve kinds
 enum : int {
-  MP_SINGTEST, MP_SINGTEST_POST, MP_FACTOR, MP_INIT, MP_INIT_RHS, MP_INIT_POST, MP_INIT_SHIFT,
-  MP_ITER, MP_ITER_B, MP_ITER_C, MP_KKT, MP_KKT_B, MP_KKT_POST,
-  MP_S0, MP_S1, MP_S2, MP_S3, MP_S4, MP_S5, MP_S6, MP_S7,
-  MP_POST_A, MP_POST_B, MP_POST_C, MP_POST_D, MP_AFF_E
+  MP_SINGTEST, MP_SINGTEST_POST, MP_FACTOR, MP_INIT, MP_ITER, MP_KKT,
+  MP_SOLVE_HEAD, MP_SOLVE_MAT, MP_SOLVE_TAIL
 };
+enum : int { RET_INIT, RET_KKT, RET_AFFINE, RET_COMBINED };
 
 template <int NQ, int NP, int MQ>
 struct Small {
@@ -346,6 +350,7 @@ struct Small {
   // (0 POC, 1 SOC head, 2 SOC tail, 3 none), cone offset, scan segment
   // start / last lane within the slot
   int ci[2], kd[2], eo[2], ssl[2], sle[2];
+  bool spn[2];  // the lane's cone spans both slots
   STAMP_DECL
 
   AD G[NP][NQ];  // AGPR-resident
@@ -376,6 +381,9 @@ struct Small {
       }
       LDS(O_RC + i) = (double)code;
     }
+    // segment partials: entry (v, c, slot) is written only when cone c meets the
+    // slot, the same for every problem of the launch; the rest stays zero
+    for (int e = lane; e < O_TOTC - O_PART; e += 64) LDS(O_PART + e) = 0.0;
     SYNC();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -390,6 +398,7 @@ struct Small {
       eo[s] = o;
       const int st = o > 64 * s ? o : 64 * s;
       const int en = (o + d) < 64 * (s + 1) ? (o + d) : 64 * (s + 1);
+      spn[s] = ev && o < 64 && o + d > 64;
       ssl[s] = ev ? st - 64 * s : lane;
       sle[s] = ev ? en - 1 - 64 * s : -1;
     }
@@ -441,277 +450,419 @@ struct Small {
       LDS(CA + i) = 1.0;
       LDS(CBV + i) = 0.0;
     }
-    if (lane < nc) {
-      LDS(O_MU + lane) = 1.0;
-      LDS(O_I1 + lane) = 0.5;
-    }
     for (int e = lane; e < NCS * NPAD; e += 64) LDS(O_U + e) = 0.0;
+    if (lane < nc) {  // W = I, lambda = e: mu = wbar_0 = lambda_0 = 1, wbar_1 = lambda_1 = 0
+      const int c = lane;
+      LDS(cc(CC_MU, c)) = 1.0;
+      LDS(cc(CC_IMU, c)) = 1.0;
+      LDS(cc(CC_WB0, c)) = 1.0;
+      LDS(cc(CC_I1, c)) = 0.5;
+      LDS(cc(CC_W2, c)) = 0.0;
+      LDS(cc(CC_L0, c)) = 1.0;
+      LDS(cc(CC_AA, c)) = 1.0;
+      LDS(cc(CC_IAA, c)) = 1.0;
+      LDS(cc(CC_IL0, c)) = 1.0;
+      LDS(cc(CC_IL0AA, c)) = 1.0;
+      LDS(cc(CC_SA, c)) = 1.0;
+      LDS(cc(CC_SAL, c)) = 0.5;
+    }
     SYNC();
   }
 
   // ------------------------------------------------------ cone vector ops
-  // scale!/iscale! (scalings.jl:112-173), iprod!/vprod! (vectors.jl:58-125),
-  // compute_scaling (scalings.jl:22-99), compute_step/scmax (mats.jl:30-86,
-  // in two rounds STEP1/STEP2), max_step (mats.jl:1-28).  a, b, o1, o2 are
-  // LDS offsets of k-vectors.  Exactly one instance (called from run()).
-  __device__ __forceinline__ VopResult vop(int op, int a_, int b_, int o1, int o2) {
+  // The k-vector lives in two 64-element slots (element i = 64 s + lane).  Every
+  // SOC operation of the reference (scale!/iscale!, iprod!/vprod!, the SOC
+  // branch of compute_scaling, scmax) needs one or two per-cone dot products;
+  // they come from cone_reduce, and each op below is straight-line code over
+  // registers: the values a cone head holds (x_0, the cone constants) are
+  // recomputed or read by every lane of the cone instead of being broadcast.
+
+  // Per-cone (segmented) reduction of NV values per slot.  v[s][q] holds the
+  // lane's contribution for element 64 s + lane; on return every lane of a cone
+  // holds the cone total -- a sum, or a max for the values flagged in MX.  DPP
+  // inclusive scan inside each slot, then the segment-end lanes hand their
+  // partials over through LDS (a cone may span both slots).
+  template <int NV, unsigned MX>
+  __device__ __forceinline__ void cone_reduce(double (&v)[2][NV]) {
     LANE_IDS();
-    double v[2][3];
-    bool mxp = false;
-    int nvals = 1;
-    VopResult R = {0.0, 0.0, 0};
+    const int rl = lane & 15;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (64 * s >= k) continue;
+      const int st = ssl[s];
+#define SOCP_SCAN_STEP(CTRL, RM, OK)                             \
+  {                                                              \
+    const bool ok_ = (OK);                                       \
+    _Pragma("unroll") for (int q = 0; q < NV; ++q) {             \
+      const double y = dpp<CTRL, RM>(v[s][q]);                   \
+      const double r = ((MX >> q) & 1) ? fmax(v[s][q], y) : v[s][q] + y; \
+      v[s][q] = ok_ ? r : v[s][q];                               \
+    }                                                            \
+  }
+      SOCP_SCAN_STEP(0x111, 0xF, rl >= 1 && lane - 1 >= st)
+      SOCP_SCAN_STEP(0x112, 0xF, rl >= 2 && lane - 2 >= st)
+      SOCP_SCAN_STEP(0x114, 0xF, rl >= 4 && lane - 4 >= st)
+      SOCP_SCAN_STEP(0x118, 0xF, rl >= 8 && lane - 8 >= st)
+      SOCP_SCAN_STEP(0x142, 0xA, ((lane >> 4) & 1) && ((lane & ~15) - 1 >= st))
+      SOCP_SCAN_STEP(0x143, 0xC, lane >= 32 && 31 >= st)
+#undef SOCP_SCAN_STEP
+      if (lane == sle[s]) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) LDS(O_PART + (q * NCS + ci[s]) * 2 + s) = v[s][q];
+      }
+    }
+    SYNC();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (64 * s >= k) continue;
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        const double p0 = LDS(O_PART + (q * NCS + ci[s]) * 2), p1 = LDS(O_PART + (q * NCS + ci[s]) * 2 + 1);
+        const double both = ((MX >> q) & 1) ? fmax(p0, p1) : p0 + p1;
+        v[s][q] = spn[s] ? both : (s == 0 ? p0 : p1);
+      }
+    }
+  }
+
+  __device__ __forceinline__ double ccv(int q, int c) const { return LDS(cc(q, c)); }
+
+  // max over cones of the value the first lane of every cone stored at O_TOTC + off
+  __device__ __forceinline__ double cone_max(int off) const {
+    double t = -INFINITY;
+    for (int c = 0; c < nc; ++c) t = fmax(t, LDS(O_TOTC + off + c));
+    return t;
+  }
+
+  // compute_scaling (scalings.jl:22-110) and ds = lam o lam (solver.jl:120).
+  // Writes WB (wbar / sqrt(s/z)), LAM, the X = W^-1 G row coefficients CA, CBV,
+  // DS (write_ds: the iteration's lam o lam; the KKT entry keeps its ds), and the
+  // per-cone constants; ll = lam'lam.  Returns the DomainError flag;
+  // dm_aa flags a negative lambda_0^2 - |lambda_1|^2 (scmax's sqrt, mats.jl:66),
+  // which the reference raises later, at compute_step.
+  __device__ __forceinline__ bool scaling_op(double& ll, bool& dm_aa, bool write_ds) {
+    LANE_IDS();
+    double v[2][3], zi[2], si[2], z0[2], s0[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane, o = eo[s];
+      zi[s] = LDS(Z_ + i);
+      si[s] = LDS(S_ + i);
+      z0[s] = LDS(Z_ + o);
+      s0[s] = LDS(S_ + o);
+      const bool tail = kd[s] == 2;
+      v[s][0] = tail ? zi[s] * zi[s] : 0.0;
+      v[s][1] = tail ? si[s] * si[s] : 0.0;
+      v[s][2] = tail ? zi[s] * si[s] : 0.0;
+    }
+    cone_reduce<3, 0>(v);
+    bool dm = false;
+    double li[2], wbi[2], l0v[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      li[s] = wbi[s] = l0v[s] = 0.0;
+      if (64 * s >= k) continue;
+      const int i = 64 * s + lane, c = ci[s];
+      const bool hd = kd[s] == 1, poc = kd[s] == 0, real = kd[s] != 3;
+      // POC (scalings.jl:22-30)
+      const double r = si[s] / zi[s], pr = si[s] * zi[s], ir = zi[s] / si[s];
+      const bool dp = (r < 0.0) || (pr < 0.0) || (ir < 0.0);
+      // SOC (scalings.jl:32-99)
+      const double onrmz = z0[s] * z0[s] - v[s][0], onrms = s0[s] * s0[s] - v[s][1];
+      const double nrmz = sqrt(onrmz), nrms = sqrt(onrms);
+      const double fz = 1.0 / nrmz, fs = 1.0 / nrms;
+      const double zb0 = z0[s] * fz, sb0 = s0[s] * fs;
+      const double nsum = zb0 * sb0 + v[s][2] * fz * fs;
+      const double garg = (1.0 + nsum) / 2.0;
+      const double gamma = sqrt(garg);
+      const double fg = 1.0 / (2.0 * gamma);
+      const double wb0 = (sb0 + zb0) * fg;
+      const double zbi = zi[s] * fz, sbi = si[s] * fs;
+      const double ratio = nrms / nrmz, prod = nrms * nrmz;
+      const double mu = sqrt(ratio);
+      const double tmv1 = sqrt(prod);
+      const double mult = tmv1 / (zb0 + sb0 + 2.0 * gamma);
+      const double l0 = gamma * tmv1;
+      const double im = 1.0 / mu;
+      const bool ds_ = (onrmz < 0.0) || (onrms < 0.0) || (garg < 0.0) || (ratio < 0.0) || (prod < 0.0);
+      const double wsoc = hd ? wb0 : (sbi - zbi) * fg;
+      const double lsoc = hd ? l0 : (sbi * (gamma + zb0) + zbi * (gamma + sb0)) * mult;
+      dm |= real && (poc ? dp : ds_);
+      wbi[s] = poc ? sqrt(r) : wsoc;
+      li[s] = poc ? sqrt(pr) : lsoc;
+      l0v[s] = l0;
+      if (real) {
+        LDS(WB + i) = wbi[s];
+        LDS(LAM + i) = li[s];
+        LDS(CA + i) = poc ? sqrt(ir) : (hd ? -im : im);
+        LDS(CBV + i) = poc ? 0.0 : (hd ? -(1.0 + wb0) * im : wsoc * im);
+      }
+      if (hd) {
+        LDS(cc(CC_MU, c)) = mu;
+        LDS(cc(CC_IMU, c)) = im;
+        LDS(cc(CC_WB0, c)) = wb0;
+        LDS(cc(CC_I1, c)) = 1.0 / (1.0 + wb0);
+      }
+    }
+    // lam o lam (vprod!, vectors.jl:58-75), |lam_1|^2 (iprod!'s a), |wbar_1|^2
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bool tail = kd[s] == 2;
+      v[s][0] = kd[s] != 3 ? li[s] * li[s] : 0.0;
+      v[s][1] = tail ? li[s] * li[s] : 0.0;
+      v[s][2] = tail ? wbi[s] * wbi[s] : 0.0;
+    }
+    cone_reduce<3, 0>(v);
+    bool da = false;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (64 * s >= k) continue;
+      const int i = 64 * s + lane, c = ci[s];
+      const bool hd = kd[s] == 1, poc = kd[s] == 0;
+      const double l0 = l0v[s];
+      if (write_ds && kd[s] != 3) LDS(DS + i) = poc ? li[s] * li[s] : (hd ? v[s][0] : l0 * li[s] + l0 * li[s]);
+      if (i == eo[s] && kd[s] != 3) LDS(O_TOTC + c) = v[s][0];
+      if (hd) {
+        const double aa = l0 * l0 - v[s][1];
+        da |= aa < 0.0;
+        const double sa = 1.0 / sqrt(aa);
+        LDS(cc(CC_W2, c)) = v[s][2];
+        LDS(cc(CC_L0, c)) = l0;
+        LDS(cc(CC_AA, c)) = aa;
+        LDS(cc(CC_IAA, c)) = 1.0 / aa;
+        LDS(cc(CC_IL0, c)) = 1.0 / l0;
+        LDS(cc(CC_IL0AA, c)) = 1.0 / (l0 * aa);
+        LDS(cc(CC_SA, c)) = sa;
+        LDS(cc(CC_SAL, c)) = 1.0 / (sa * l0 + 1.0);
+      }
+    }
+    SYNC();
+    double t = 0.0;
+    for (int c = 0; c < nc; ++c) t += LDS(O_TOTC + c);
+    ll = t;
+    dm_aa = __any(da);
+    return __any(dm);
+  }
+
+  // First half of solve_kkt(::DenseSolver) (densesolver.jl:61-66):
+  //   k0 = lam^-1 o ds (iprod!), k1 = W k0 (scale!), k2 = dz - k1,
+  //   t2 = iWiW k2 = W^-1 (W^-1 k2): the second W^-1 reuses the first one's
+  //   cone reduction (wbar_1'(W^-1 x)_1 follows from wbar_1'x_1 and |wbar_1|^2).
+  // In: DS, DZ.  Out: K0, K2, T2.
+  __device__ __forceinline__ void solve_head() {
+    LANE_IDS();
+    double v[2][1], x[2], lam[2], wb[2], x0[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int i = 64 * s + lane;
-      const bool tail = kd[s] == 2, hd = kd[s] == 1, poc = kd[s] == 0;
-      double v0 = 0.0, v1 = 0.0, v2 = 0.0;
-      if (op == VOP_SCALE || op == VOP_ISCALE) {
-        if (tail) v0 = LDS(WB + i) * LDS(a_ + i);
-      } else if (op == VOP_PAIR) {
-        if (tail) {
-          v0 = LDS(WB + i) * LDS(a_ + i);
-          v1 = LDS(WB + i) * LDS(b_ + i);
-        }
-      } else if (op == VOP_IPROD) {
-        const double li = LDS(LAM + i);
-        if (tail) {
-          v0 = li * li;
-          v1 = LDS(a_ + i) * li;
-        }
-      } else if (op == VOP_VPROD) {
-        if (tail || hd) v0 = LDS(a_ + i) * LDS(b_ + i);
-      } else if (op == VOP_SCALING) {  // a = z, b = s
-        if (tail) {
-          const double zi = LDS(a_ + i), si = LDS(b_ + i);
-          v0 = zi * zi;
-          v1 = si * si;
-          v2 = zi * si;
-        }
-      } else if (op == VOP_STEP1) {  // scmax(l, a), scmax(l, b): first round
-        const double li = LDS(LAM + i);
-        if (tail) {
-          v0 = li * li;
-          v1 = li * LDS(a_ + i);
-          v2 = li * LDS(b_ + i);
-        } else if (poc) {
-          v0 = -LDS(a_ + i) / li;
-          v1 = -LDS(b_ + i) / li;
-        }
-      } else if (op == VOP_STEP2) {  // second round: r2s of both directions
-        if (tail) {
-          const int o = eo[s], c = ci[s];
-          const double av = LDS(O_CST + c * 4), ra = LDS(O_CST + c * 4 + 1),
-                       rb = LDS(O_CST + c * 4 + 2);
-          const double l0 = LDS(LAM + o), li = LDS(LAM + i);
-          const double csa = (ra + LDS(a_ + o)) / (av * l0 + 1.0);
-          const double csb = (rb + LDS(b_ + o)) / (av * l0 + 1.0);
-          const double qa = av * (LDS(a_ + i) - csa * av * li);
-          const double qb = av * (LDS(b_ + i) - csb * av * li);
-          v0 = qa * qa;
-          v1 = qb * qb;
-        }
-      } else if (op == VOP_MAXSTEP) {  // max_step(-a), max_step(a)
-        const double xi = LDS(a_ + i);
-        if (tail) v0 = xi * xi;
-        if (poc) {
-          v0 = xi;
-          v1 = -xi;
-        }
-      }
-      v[s][0] = v0;
-      v[s][1] = v1;
-      v[s][2] = v2;
+      x[s] = LDS(DS + i);
+      x0[s] = LDS(DS + eo[s]);
+      lam[s] = LDS(LAM + i);
+      wb[s] = LDS(WB + i);
+      v[s][0] = kd[s] == 2 ? lam[s] * x[s] : 0.0;
     }
-    if (op == VOP_PAIR || op == VOP_IPROD || op == VOP_STEP2 || op == VOP_MAXSTEP) nvals = 2;
-    if (op == VOP_SCALING || op == VOP_STEP1) nvals = 3;
-    mxp = (op == VOP_STEP1 || op == VOP_MAXSTEP);
-    // ---- per-cone segmented reduction (DPP scan per slot, then per-cone totals)
+    cone_reduce<1, 0>(v);
+    double k0[2], k00[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      if (64 * s < k) {
-        const bool mx = mxp && kd[s] == 0;
-        if (nvals == 1) {
-          double x[1] = {v[s][0]};
-          dpp_scan<1>(x, lane, ssl[s], mx);
-          v[s][0] = x[0];
-        } else if (nvals == 2) {
-          double x[2] = {v[s][0], v[s][1]};
-          dpp_scan<2>(x, lane, ssl[s], mx);
-          v[s][0] = x[0];
-          v[s][1] = x[1];
-        } else {
-          dpp_scan<3>(v[s], lane, ssl[s], mx);
-        }
-        if (lane == sle[s]) {
-#pragma unroll
-          for (int q = 0; q < 3; ++q) LDS(O_PART + (s * NCS + ci[s]) * 4 + q) = v[s][q];
-        }
-      }
+      const int c = ci[s];
+      const double t = v[s][0];
+      k00[s] = (x0[s] * ccv(CC_L0, c) - t) * ccv(CC_IAA, c);
+      const double tl = -(x0[s] * lam[s] * ccv(CC_IAA, c)) + x[s] * ccv(CC_IL0, c) + lam[s] * t * ccv(CC_IL0AA, c);
+      k0[s] = kd[s] == 0 ? x[s] / lam[s] : (kd[s] == 1 ? k00[s] : tl);
+      v[s][0] = kd[s] == 2 ? wb[s] * k0[s] : 0.0;
     }
-    SYNC();
-    if (lane < nc) {
-      const int c = lane;
-      const int o = (int)LDS(O_COFF + c), d = (int)LDS(O_CDIM + c);
-      const bool mx = mxp && (int)LDS(O_CKIND + c) == POC_K;
-      const int s0 = o >> 6, s1 = (o + d - 1) >> 6;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        double t = LDS(O_PART + (s0 * NCS + c) * 4 + q);
-        if (s1 > s0) {
-          const double u = LDS(O_PART + (s1 * NCS + c) * 4 + q);
-          t = mx ? fmax(t, u) : t + u;
-        }
-        LDS(O_TOT + c * 4 + q) = t;
-      }
-    }
-    SYNC();
-    // ---- outputs
-    bool dm = false;
-    double best = -INFINITY, bp = -INFINITY;
+    cone_reduce<1, 0>(v);
+    double k2[2], k20[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane, c = ci[s];
+      const double del = v[s][0], mu = ccv(CC_MU, c), wb0 = ccv(CC_WB0, c);
+      const double k10 = mu * (wb0 * k00[s] + del);
+      const double k1 = kd[s] == 0 ? wb[s] * k0[s] : (kd[s] == 1 ? k10 : mu * (k0[s] + (k00[s] + del * ccv(CC_I1, c)) * wb[s]));
+      k2[s] = LDS(DZ + i) - k1;
+      k20[s] = LDS(DZ + eo[s]) - k10;
+      if (kd[s] != 3) {
+        LDS(K0 + i) = k0[s];
+        LDS(K2 + i) = k2[s];
+      }
+      v[s][0] = kd[s] == 2 ? wb[s] * k2[s] : 0.0;
+    }
+    cone_reduce<1, 0>(v);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane, c = ci[s];
+      const double a1 = v[s][0], im = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
+      const double cy = a1 * i1 - k20[s];
+      const double y0 = im * (wb0 * k20[s] - a1);
+      const double y = kd[s] == 1 ? y0 : im * (k2[s] + cy * wb[s]);
+      const double a2 = im * (a1 + cy * ccv(CC_W2, c));
+      const double zs = kd[s] == 1 ? im * (wb0 * y0 - a2) : im * (y + (a2 * i1 - y0) * wb[s]);
+      const double ca = LDS(CA + i);
+      if (kd[s] != 3) LDS(T2 + i) = kd[s] == 0 ? ca * (ca * k2[s]) : zs;
+    }
+    SYNC();
+  }
+
+  // Second half of solve_kkt (densesolver.jl:83-88): cz = iWiW k1 = W^-1 (W^-1 k1),
+  // k0 -= W cz (W cz = W^-1 k1), cs = W k0.  With do_step, compute_step
+  // (mats.jl:30-40) of the direction (solver.jl:128-130, 143-145) follows:
+  // kt3 = W rz and kt2 = W^-1 rs are W^-1 k1 and the updated k0 exactly, so they
+  // are taken from here.  In: K1 (= G cx - k2), K0.  Out: RZ, RS, and with
+  // do_step T1 = kt3, K0 = kt2, the step length (dom: DomainError).
+  __device__ __forceinline__ double solve_tail(bool do_step, bool dm_aa, int& dom) {
+    LANE_IDS();
+    double v[2][1], k1[2], k10[2], wb[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane;
+      k1[s] = LDS(K1 + i);
+      k10[s] = LDS(K1 + eo[s]);
+      wb[s] = LDS(WB + i);
+      v[s][0] = kd[s] == 2 ? wb[s] * k1[s] : 0.0;
+    }
+    cone_reduce<1, 0>(v);
+    double y[2], y0v[2], kn[2], kn0[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane, c = ci[s];
+      const double a1 = v[s][0], im = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
+      const double ca = LDS(CA + i);
+      const double cy = a1 * i1 - k10[s];
+      const double y0 = im * (wb0 * k10[s] - a1);
+      y[s] = kd[s] == 0 ? ca * k1[s] : (kd[s] == 1 ? y0 : im * (k1[s] + cy * wb[s]));
+      const double a2 = im * (a1 + cy * ccv(CC_W2, c));
+      const double zs = kd[s] == 1 ? im * (wb0 * y0 - a2) : im * (y[s] + (a2 * i1 - y0) * wb[s]);
+      if (kd[s] != 3) LDS(RZ + i) = kd[s] == 0 ? ca * y[s] : zs;
+      y0v[s] = y0;
+      kn[s] = LDS(K0 + i) - y[s];
+      kn0[s] = LDS(K0 + eo[s]) - y0;
+      v[s][0] = kd[s] == 2 ? wb[s] * kn[s] : 0.0;
+    }
+    cone_reduce<1, 0>(v);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane, c = ci[s];
+      const double del = v[s][0], mu = ccv(CC_MU, c), wb0 = ccv(CC_WB0, c);
+      const double cs = kd[s] == 0 ? wb[s] * kn[s]
+                                   : (kd[s] == 1 ? mu * (wb0 * kn0[s] + del)
+                                                 : mu * (kn[s] + (kn0[s] + del * ccv(CC_I1, c)) * wb[s]));
+      if (kd[s] != 3) LDS(RS + i) = cs;
+    }
+    if (!do_step) {
+      SYNC();
+      return 0.0;
+    }
+    // scmax (mats.jl:42-86) of kt3 = y and kt2 = kn
+    double w[2][4], lam[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane;
+      if (kd[s] != 3) {
+        LDS(T1 + i) = y[s];
+        LDS(K0 + i) = kn[s];
+      }
+      lam[s] = LDS(LAM + i);
+      const bool tail = kd[s] == 2, poc = kd[s] == 0;
+      w[s][0] = tail ? lam[s] * y[s] : 0.0;
+      w[s][1] = tail ? lam[s] * kn[s] : 0.0;
+      w[s][2] = poc ? -y[s] / lam[s] : -INFINITY;
+      w[s][3] = poc ? -kn[s] / lam[s] : -INFINITY;
+    }
+    cone_reduce<4, 0xC>(w);
+    double q[2][2], r1y[2], r1k[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = ci[s];
+      const double sa = ccv(CC_SA, c), l0 = ccv(CC_L0, c), sal = ccv(CC_SAL, c);
+      r1y[s] = sa * l0 * y0v[s] - sa * w[s][0];
+      r1k[s] = sa * l0 * kn0[s] - sa * w[s][1];
+      const double cyy = (r1y[s] + y0v[s]) * sal, cyk = (r1k[s] + kn0[s]) * sal;
+      const double qy = sa * (y[s] - cyy * sa * lam[s]), qk = sa * (kn[s] - cyk * sa * lam[s]);
+      q[s][0] = kd[s] == 2 ? qy * qy : 0.0;
+      q[s][1] = kd[s] == 2 ? qk * qk : 0.0;
+    }
+    cone_reduce<2, 0>(q);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = ci[s];
+      if (64 * s >= k || kd[s] == 3 || 64 * s + lane != eo[s]) continue;
+      const double sa = ccv(CC_SA, c);
+      const double vy = sqrt(q[s][0]) - sa * r1y[s], vk = sqrt(q[s][1]) - sa * r1k[s];
+      LDS(O_TOTC + c) = kd[s] == 0 ? fmax(w[s][2], w[s][3]) : fmax(vy, vk);
+    }
+    SYNC();
+    dom = dm_aa ? 1 : 0;
+    const double t = fmax(cone_max(0), 0.0);
+    return (t == 0.0) ? 1.0 : fmin(1.0, 1.0 / t);
+  }
+
+  // rho, sigma, mu (solver.jl:132-134) and the corrector right-hand side
+  // (:136-140): kt1 = kt2 o kt3, ds += sigma mu e - kt1, dx, dy, dz *= 1 - sigma.
+  // In: K0 (kt2), T1 (kt3), DS, DZ, RD, RP.
+  __device__ __forceinline__ void affine_post(double tstep, double ll) {
+    LANE_IDS();
+    double v[2][1], a2[2], a3[2], a20[2], a30[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane;
+      a2[s] = LDS(K0 + i);
+      a3[s] = LDS(T1 + i);
+      a20[s] = LDS(K0 + eo[s]);
+      a30[s] = LDS(T1 + eo[s]);
+      v[s][0] = kd[s] != 3 ? a2[s] * a3[s] : 0.0;
+    }
+    cone_reduce<1, 0>(v);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      if (64 * s < k && kd[s] != 3 && 64 * s + lane == eo[s]) LDS(O_TOTC + ci[s]) = v[s][0];
+    SYNC();
+    double kk = 0.0;
+    for (int c = 0; c < nc; ++c) kk += LDS(O_TOTC + c);
+    const double t = tstep;
+    const double rho = 1.0 - t - t * t * kk / ll;
+    const double cr = isnan(rho) ? rho : (rho < 0.0 ? 0.0 : (rho > 1.0 ? 1.0 : rho));
+    const double sig = ipow(cr, a.sigma_exp);  // max(0,min(1,rho))^3 (solver.jl:133)
+    const double mu_ipm = ll / a.deg;
+    const double scf = 1.0 - sig;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane;
       if (kd[s] == 3) continue;
-      const int i = 64 * s + lane, c = ci[s], o = eo[s];
-      const bool hd = kd[s] == 1, poc = kd[s] == 0;
-      const double t0 = LDS(O_TOT + c * 4), t1 = LDS(O_TOT + c * 4 + 1), t2 = LDS(O_TOT + c * 4 + 2);
-      if (op == VOP_SCALE || op == VOP_ISCALE || op == VOP_PAIR) {
-        const double wi = LDS(WB + i), xi = LDS(a_ + i);
-        double r;
-        if (poc) {
-          r = (op == VOP_ISCALE) ? (1.0 / wi) * xi : wi * xi;
-        } else {
-          const double mu = LDS(O_MU + c), wb0 = LDS(WB + o), x0 = LDS(a_ + o);
-          if (op != VOP_ISCALE) {
-            const double cst = x0 + t0 / (1.0 + wb0);
-            r = hd ? mu * (wb0 * x0 + t0) : mu * (xi + cst * wi);
-          } else {
-            const double cst = -x0 + t0 / (1.0 + wb0);
-            const double im = 1.0 / mu;
-            r = hd ? im * (wb0 * x0 - t0) : im * (xi + cst * wi);
-          }
-        }
-        if (op == VOP_PAIR) {
-          const double x2 = LDS(b_ + i);
-          double r2;
-          if (poc) {
-            r2 = (1.0 / wi) * x2;
-          } else {
-            const double mu = LDS(O_MU + c), wb0 = LDS(WB + o), x0 = LDS(b_ + o);
-            const double cst = -x0 + t1 / (1.0 + wb0);
-            const double im = 1.0 / mu;
-            r2 = hd ? im * (wb0 * x0 - t1) : im * (x2 + cst * wi);
-          }
-          LDS(o2 + i) = r2;
-        }
-        LDS(o1 + i) = r;
-      } else if (op == VOP_IPROD) {
-        const double vi = LDS(a_ + i), li = LDS(LAM + i);
-        double r;
-        if (poc) {
-          r = vi / li;
-        } else {
-          const double l0 = LDS(LAM + o), v0 = LDS(a_ + o);
-          const double aa = l0 * l0 - t0;
-          r = hd ? v0 * l0 / aa - t1 / aa : -(v0 * li / aa) + vi / l0 + li * t1 / (l0 * aa);
-        }
-        LDS(o1 + i) = r;
-      } else if (op == VOP_VPROD) {
-        const double ui = LDS(a_ + i), vi = LDS(b_ + i);
-        double r;
-        if (poc)
-          r = ui * vi;
-        else
-          r = hd ? t0 : LDS(a_ + o) * vi + LDS(b_ + o) * ui;
-        LDS(o1 + i) = r;
-      } else if (op == VOP_SCALING) {
-        // compute_scaling (scalings.jl:22-99) -> lam, wb, mu, 1/(1+wb0), and the
-        // X = W^-1 G row coefficients: X[i,:] = ca[i] G[i,:] + cb[i] U[cone(i),:]
-        const double zi = LDS(a_ + i), si = LDS(b_ + i);
-        double wbi, li, cai, cbi;
-        if (poc) {
-          const double r = si / zi, pr = si * zi, ir = zi / si;
-          dm |= (r < 0.0) || (pr < 0.0) || (ir < 0.0);
-          wbi = sqrt(r);
-          li = sqrt(pr);
-          cai = sqrt(ir);
-          cbi = 0.0;
-        } else {
-          const double z0 = LDS(a_ + o), s0 = LDS(b_ + o);
-          const double onrmz = z0 * z0 - t0, onrms = s0 * s0 - t1;
-          dm |= (onrmz < 0.0) || (onrms < 0.0);
-          const double nrmz = sqrt(onrmz), nrms = sqrt(onrms);
-          const double fz = 1.0 / nrmz, fs = 1.0 / nrms;
-          const double zb0 = z0 * fz, sb0 = s0 * fs;
-          const double nsum = zb0 * sb0 + t2 * fz * fs;
-          const double garg = (1.0 + nsum) / 2.0;
-          dm |= garg < 0.0;
-          const double gamma = sqrt(garg);
-          const double fg = 1.0 / (2.0 * gamma);
-          const double wb0 = (sb0 + zb0) * fg;
-          const double zbi = zi * fz, sbi = si * fs;
-          wbi = hd ? wb0 : (sbi - zbi) * fg;
-          const double ratio = nrms / nrmz, prod = nrms * nrmz;
-          dm |= (ratio < 0.0) || (prod < 0.0);
-          const double mu = sqrt(ratio);
-          const double tmv1 = sqrt(prod);
-          const double mult = tmv1 / (zb0 + sb0 + 2.0 * gamma);
-          li = hd ? gamma * tmv1 : (sbi * (gamma + zb0) + zbi * (gamma + sb0)) * mult;
-          const double im = 1.0 / mu;
-          cai = hd ? -im : im;
-          cbi = hd ? -(1.0 + wb0) * im : wbi * im;
-          if (hd) {
-            LDS(O_MU + c) = mu;
-            LDS(O_I1 + c) = 1.0 / (1.0 + wb0);
-          }
-        }
-        LDS(WB + i) = wbi;
-        LDS(LAM + i) = li;
-        LDS(CA + i) = cai;
-        LDS(CBV + i) = cbi;
-      } else if (op == VOP_STEP1) {
-        if (hd) {
-          const double l0 = LDS(LAM + o);
-          const double ai = l0 * l0 - t0;
-          dm |= ai < 0.0;
-          const double av = 1.0 / sqrt(ai);
-          LDS(O_CST + c * 4) = av;
-          LDS(O_CST + c * 4 + 1) = av * l0 * LDS(a_ + o) - av * t1;
-          LDS(O_CST + c * 4 + 2) = av * l0 * LDS(b_ + o) - av * t2;
-        } else if (poc && i == o) {
-          LDS(O_CST + c * 4 + 3) = fmax(t0, t1);
-        }
-      } else if (op == VOP_STEP2) {
-        if (hd) {
-          const double av = LDS(O_CST + c * 4);
-          const double va = sqrt(t0) - av * LDS(O_CST + c * 4 + 1);
-          const double vb = sqrt(t1) - av * LDS(O_CST + c * 4 + 2);
-          best = fmax(best, fmax(va, vb));
-        } else if (poc && i == o) {
-          best = fmax(best, LDS(O_CST + c * 4 + 3));
-        }
-      } else if (op == VOP_MAXSTEP) {
-        if (poc && i == o) {
-          best = fmax(best, t0);
-          bp = fmax(bp, t1);
-        } else if (hd) {
-          const double nr = sqrt(t0), x0 = LDS(a_ + o);
-          best = fmax(best, nr + x0);
-          bp = fmax(bp, nr - x0);
-        }
-      }
+      const double kt1 = kd[s] == 0 ? a2[s] * a3[s] : (kd[s] == 1 ? v[s][0] : a20[s] * a3[s] + a30[s] * a2[s]);
+      const double e = kd[s] == 2 ? 0.0 : 1.0;
+      LDS(DS + i) = LDS(DS + i) + (sig * mu_ipm * e - kt1);
+      LDS(DZ + i) = LDS(DZ + i) * scf;
+    }
+    for (int j = lane; j < n; j += 64) LDS(RD + j) = LDS(RD + j) * scf;
+    for (int i = lane; i < m; i += 64) LDS(RP + i) = LDS(RP + i) * scf;
+    SYNC();
+  }
+
+  // max_step(-iz), max_step(iz) (mats.jl:1-28) for the initial shift (solver.jl:88-101)
+  __device__ __forceinline__ void maxstep_op(int xv, double& alphp, double& alphd) {
+    LANE_IDS();
+    double v[2][3], x[2], x0[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane;
+      x[s] = LDS(xv + i);
+      x0[s] = LDS(xv + eo[s]);
+      v[s][0] = kd[s] == 2 ? x[s] * x[s] : 0.0;
+      v[s][1] = kd[s] == 0 ? x[s] : -INFINITY;
+      v[s][2] = kd[s] == 0 ? -x[s] : -INFINITY;
+    }
+    cone_reduce<3, 0x6>(v);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (64 * s >= k || kd[s] == 3 || 64 * s + lane != eo[s]) continue;
+      const double nr = sqrt(v[s][0]);
+      const bool poc = kd[s] == 0;
+      LDS(O_TOTC + ci[s]) = poc ? v[s][1] : nr + x0[s];
+      LDS(O_TOTC + NCS + ci[s]) = poc ? v[s][2] : nr - x0[s];
     }
     SYNC();
-    R.dom = __any(dm) ? 1 : 0;
-    if (op == VOP_STEP2) {
-      double t = wmax(best);
-      if (isnan(t)) t = -INFINITY;
-      t = fmax(t, 0.0);
-      R.r0 = (t == 0.0) ? 1.0 : fmin(1.0, 1.0 / t);
-    } else if (op == VOP_MAXSTEP) {
-      R.r0 = wmax(best);
-      R.r1 = wmax(bp);
-    }
-    return R;
+    alphp = cone_max(0);
+    alphd = cone_max(NCS);
   }
 
   // U[c,:] = (sum_{i in cone c} w_i G[i,:]) / (1+wb0), w_head = -(1+wb0), w_tail = wb_i
@@ -740,7 +891,7 @@ struct Small {
         acc[q] += __shfl_xor(acc[q], 32);
       }
       if (g == 0) {
-        const double inv = LDS(O_I1 + c);
+        const double inv = LDS(cc(CC_I1, c));
 #pragma unroll
         for (int q = 0; q < NQ; ++q) LDS(O_U + c * NPAD + 16 * q + cl) = acc[q] * inv;
       }
@@ -1246,18 +1397,18 @@ struct Small {
   }
 
   // ------------------------------------------------------------- driver
-  // solve_socp (solver.jl:40-153) as a micro-phase loop; solve_kkt
-  // (densesolver.jl:54-90) is phases MP_S0..MP_S7, returning to `ret`.
+  // solve_socp (solver.jl:40-153) as a micro-phase loop.  solve_kkt
+  // (densesolver.jl:54-90) is MP_SOLVE_HEAD -> MP_SOLVE_MAT -> MP_SOLVE_TAIL;
+  // `ret` says which solve it is (init, KKT entry, affine, combined).
   __device__ __forceinline__ void run(int64_t p) {
     STAMP(SP_LOAD);
     dbg_p = p;
     int status = ST_MAXIT, iters = 0, it = 0;
     double nd = NAN, np_ = NAN, gap = NAN;
-    double sig = 0.0, mu_ipm = 0.0, tstep = 0.0;
-    bool fac_ident = false, fac_aa = false, dom_step = false;
+    double ll = 0.0;
+    bool fac_ident = false, fac_aa = false, dm_aa = false;
     int fret = 0, ret = 0, fst = 0;
     int after_singtest;
-    VopResult vr = {0.0, 0.0, 0};
     if (a.mode == MODE_KKT) {
       for (int i = lane; i < k; i += 64) {
         LDS(S_ + i) = a.s[p * k + i];
@@ -1291,7 +1442,6 @@ struct Small {
     bool done = false;
     while (!done) {
       LANE_IDS();
-      int op = -1, va = 0, vb = 0, vo1 = 0, vo2 = 0;
       int next = phase;
       switch (phase) {
         case MP_SINGTEST:  // Problem's `sing` (Socp.jl:49-56): is G'G positive definite?
@@ -1315,12 +1465,6 @@ struct Small {
           break;
         case MP_INIT:  // initial point: the KKT system with W = I (solver.jl:68-84)
           scaling_identity();
-          fac_ident = true;
-          fac_aa = sing;
-          fret = MP_INIT_RHS;
-          next = MP_FACTOR;
-          break;
-        case MP_INIT_RHS:
           for (int j = lane; j < n; j += 64) LDS(RD + j) = -LDS(C_ + j);
           for (int i = lane; i < m; i += 64) LDS(RP + i) = LDS(B_ + i);
           for (int i = lane; i < k; i += 64) {
@@ -1328,28 +1472,13 @@ struct Small {
             LDS(DS + i) = 0.0;
           }
           SYNC();
-          ret = MP_INIT_POST;
-          next = MP_S0;
+          fac_ident = true;
+          fac_aa = sing;
+          fret = MP_SOLVE_HEAD;
+          ret = RET_INIT;
+          next = MP_FACTOR;
           break;
-        case MP_INIT_POST:
-          op = VOP_MAXSTEP;
-          va = RZ;
-          next = MP_INIT_SHIFT;
-          break;
-        case MP_INIT_SHIFT: {  // cone shift (solver.jl:86-104)
-          const double alphp = vr.r0, alphd = vr.r1;  // max_step(-iz), max_step(iz)
-          for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(RX + j);
-          for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(RY + i);
-          for (int i = lane; i < k; i += 64) {
-            const double iz = LDS(RZ + i), e = e_of(i);
-            LDS(S_ + i) = (fabs(alphp) < a.init_eps) ? -iz : -iz + (1.0 + alphp) * e;
-            LDS(Z_ + i) = (fabs(alphd) < a.init_eps) ? iz : iz + (1.0 + alphd) * e;
-          }
-          SYNC();
-          next = MP_ITER;
-          break;
-        }
-        case MP_ITER:  // residuals (solver.jl:109-118), then compute_scaling (:106)
+        case MP_ITER: {  // residuals (solver.jl:109-118), compute_scaling (:106), exit test (:122)
           STAMP(SP_OTHER);
           residuals(nd, np_, gap);
           STAMP(SP_RESID);
@@ -1357,25 +1486,14 @@ struct Small {
             done = true;
             break;
           }
-          op = VOP_SCALING;
-          va = Z_;
-          vb = S_;
-          next = MP_ITER_B;
-          break;
-        case MP_ITER_B:
-          if (vr.dom) {
+          const bool dm = scaling_op(ll, dm_aa, true);
+          STAMP(SP_VOP);
+          if (dm) {
             status = ST_DOMAIN;
             done = true;
             break;
           }
-          op = VOP_VPROD;  // ds = lam o lam (solver.jl:120)
-          va = LAM;
-          vb = LAM;
-          vo1 = DS;
-          next = MP_ITER_C;
-          break;
-        case MP_ITER_C:
-          if (nd + np_ + gap < a.tol) {  // exit test (solver.jl:122)
+          if (nd + np_ + gap < a.tol) {
             status = ST_CONVERGED;
             done = true;
             break;
@@ -1389,145 +1507,77 @@ struct Small {
           SYNC();
           fac_ident = false;
           fac_aa = sing;
-          fret = MP_S0;
-          ret = MP_POST_A;
-          dom_step = false;
+          fret = MP_SOLVE_HEAD;
+          ret = RET_AFFINE;
           next = MP_FACTOR;
           break;
-        case MP_KKT:
-          op = VOP_SCALING;
-          va = Z_;
-          vb = S_;
-          next = MP_KKT_B;
-          break;
-        case MP_KKT_B:
-          if (vr.dom) {
+        }
+        case MP_KKT: {
+          const bool dm = scaling_op(ll, dm_aa, false);
+          if (dm) {
             status = ST_DOMAIN;
             done = true;
             break;
           }
           fac_ident = false;
           fac_aa = sing;
-          fret = MP_S0;
-          ret = MP_KKT_POST;
+          fret = MP_SOLVE_HEAD;
+          ret = RET_KKT;
           next = MP_FACTOR;
           break;
-        case MP_KKT_POST:
-          status = 0;
-          for (int j = lane; j < n; j += 64) a.cx[p * n + j] = LDS(RX + j);
-          for (int i = lane; i < m; i += 64) a.cy[p * m + i] = LDS(RY + i);
-          for (int i = lane; i < k; i += 64) {
-            a.cz[p * k + i] = LDS(RZ + i);
-            a.cs[p * k + i] = LDS(RS + i);
-          }
-          done = true;
-          break;
-        // ------------------------------- solve_kkt (densesolver.jl:54-90)
-        case MP_S0:
+        }
+        case MP_SOLVE_HEAD:
           STAMP(SP_OTHER);
-          op = VOP_IPROD;  // k0 = lam^-1 o ds
-          va = DS;
-          vo1 = K0;
-          next = MP_S1;
-          break;
-        case MP_S1:
-          op = VOP_SCALE;  // k1 = W k0
-          va = K0;
-          vo1 = K1;
-          next = MP_S2;
-          break;
-        case MP_S2:
-          for (int i = lane; i < k; i += 64) LDS(K2 + i) = LDS(DZ + i) - LDS(K1 + i);
-          SYNC();
-          op = VOP_ISCALE;
-          va = K2;
-          vo1 = T1;
-          next = MP_S3;
-          break;
-        case MP_S3:
-          op = VOP_ISCALE;  // t2 = iWiW k2
-          va = T1;
-          vo1 = T2;
-          next = MP_S4;
-          break;
-        case MP_S4:
+          solve_head();
           STAMP(SP_VOP);
-          solve_matrix_part(ret == MP_INIT_POST);
+          next = MP_SOLVE_MAT;
+          break;
+        case MP_SOLVE_MAT:
+          solve_matrix_part(ret == RET_INIT);
           STAMP(SP_SOLVE);
-          op = VOP_ISCALE;
-          va = K1;
-          vo1 = T1;
-          next = MP_S5;
+          next = MP_SOLVE_TAIL;
           break;
-        case MP_S5:
-          op = VOP_ISCALE;  // cz = iWiW k1
-          va = T1;
-          vo1 = RZ;
-          next = MP_S6;
-          break;
-        case MP_S6:
-          op = VOP_SCALE;  // k1 = W cz
-          va = RZ;
-          vo1 = K1;
-          next = MP_S7;
-          break;
-        case MP_S7:
-          for (int i = lane; i < k; i += 64) LDS(K0 + i) = LDS(K0 + i) - LDS(K1 + i);
-          SYNC();
-          op = VOP_SCALE;  // cs = W k0
-          va = K0;
-          vo1 = RS;
-          next = ret;
-          break;
-        // ------------------- step length (solver.jl:128-134, 143-146)
-        case MP_POST_A:
+        case MP_SOLVE_TAIL: {
+          const bool do_step = ret == RET_AFFINE || ret == RET_COMBINED;
+          int dom = 0;
+          const double tstep = solve_tail(do_step, dm_aa, dom);
           STAMP(SP_VOP);
-          op = VOP_PAIR;  // kt3 = W rz, kt2 = W^-1 rs
-          va = RZ;
-          vb = RS;
-          vo1 = T1;
-          vo2 = T2;
-          next = MP_POST_B;
-          break;
-        case MP_POST_B:
-          op = VOP_STEP1;
-          va = T1;
-          vb = T2;
-          next = MP_POST_C;
-          break;
-        case MP_POST_C:
-          dom_step = vr.dom != 0;
-          op = VOP_STEP2;
-          va = T1;
-          vb = T2;
-          next = MP_POST_D;
-          break;
-        case MP_POST_D: {
-          if (dom_step) {
+          if (ret == RET_KKT) {
+            status = 0;
+            for (int j = lane; j < n; j += 64) a.cx[p * n + j] = LDS(RX + j);
+            for (int i = lane; i < m; i += 64) a.cy[p * m + i] = LDS(RY + i);
+            for (int i = lane; i < k; i += 64) {
+              a.cz[p * k + i] = LDS(RZ + i);
+              a.cs[p * k + i] = LDS(RS + i);
+            }
+            done = true;
+            break;
+          }
+          if (ret == RET_INIT) {  // cone shift (solver.jl:86-104)
+            double alphp, alphd;  // max_step(-iz), max_step(iz)
+            maxstep_op(RZ, alphp, alphd);
+            for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(RX + j);
+            for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(RY + i);
+            for (int i = lane; i < k; i += 64) {
+              const double iz = LDS(RZ + i), e = e_of(i);
+              LDS(S_ + i) = (fabs(alphp) < a.init_eps) ? -iz : -iz + (1.0 + alphp) * e;
+              LDS(Z_ + i) = (fabs(alphd) < a.init_eps) ? iz : iz + (1.0 + alphd) * e;
+            }
+            SYNC();
+            next = MP_ITER;
+            break;
+          }
+          if (dom) {
             status = ST_DOMAIN;
             done = true;
             break;
           }
-          tstep = vr.r0;
-          if (ret == MP_POST_A) {  // affine direction -> centering + corrector
-            double kk = 0.0, ll = 0.0;
-            for (int i = lane; i < k; i += 64) {
-              kk += LDS(T2 + i) * LDS(T1 + i);
-              ll += LDS(LAM + i) * LDS(LAM + i);
-            }
-            kk = wsum(kk);
-            ll = wsum(ll);
-            const double t = tstep;
-            const double rho = 1.0 - t - t * t * kk / ll;
-            const double cr = isnan(rho) ? rho : (rho < 0.0 ? 0.0 : (rho > 1.0 ? 1.0 : rho));
-            sig = ipow(cr, a.sigma_exp);  // max(0,min(1,rho))^3 (solver.jl:133)
-            mu_ipm = ll / a.deg;
-            op = VOP_VPROD;  // kt1 = kt2 o kt3
-            va = T2;
-            vb = T1;
-            vo1 = K0;
-            next = MP_AFF_E;
-          } else {  // combined direction -> step and update (solver.jl:143-150)
+          if (ret == RET_AFFINE) {  // centering + corrector, then the combined solve
+            affine_post(tstep, ll);
+            STAMP(SP_STEP);
+            ret = RET_COMBINED;
+            next = MP_SOLVE_HEAD;
+          } else {  // combined direction: step and update (solver.jl:143-150)
             const double stp = tstep * a.step;
             for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(X_ + j) + LDS(RX + j) * stp;
             for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(Y_ + i) + LDS(RY + i) * stp;
@@ -1542,32 +1592,12 @@ struct Small {
           }
           break;
         }
-        case MP_AFF_E: {  // ds += sig*mu*e - kt2 o kt3; dx,dy,dz *= 1-sig (solver.jl:136-140)
-          const double scf = 1.0 - sig;
-          for (int i = lane; i < k; i += 64) {
-            const double kt2 = sig * mu_ipm * e_of(i);
-            LDS(DS + i) = LDS(DS + i) + (kt2 - LDS(K0 + i));
-            LDS(DZ + i) = LDS(DZ + i) * scf;
-          }
-          for (int j = lane; j < n; j += 64) LDS(RD + j) = LDS(RD + j) * scf;
-          for (int i = lane; i < m; i += 64) LDS(RP + i) = LDS(RP + i) * scf;
-          SYNC();
-          ret = MP_POST_A + 100;  // marks the combined pass
-          next = MP_S0;
-          break;
-        }
         default:
           done = true;
           break;
       }
       if (done) break;
-      op = uni(op);
-      if (op >= 0) {
-        vr = vop(op, uni(va), uni(vb), uni(vo1), uni(vo2));
-        STAMP(SP_VOP);
-      }
-      // the combined-pass marker routes the end of the second solve to MP_POST_A
-      phase = uni((next == MP_POST_A + 100) ? MP_POST_A : next);
+      phase = uni(next);
     }
     if (a.mode == MODE_KKT) {
       if (lane == 0) a.status[p] = status;

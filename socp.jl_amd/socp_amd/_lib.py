@@ -64,6 +64,14 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"libsocp.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    # One HIP runtime per process: torch ships its own libamdhip64 (same soname
+    # as /opt/rocm's).  Loading torch first makes libsocp bind to that copy, so
+    # device pointers, streams and contexts are shared; loading libsocp first
+    # would bring up a second runtime and torch would then see no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, i32p, dp, u8p = C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p
     L.socp_last_error.restype = C.c_char_p
