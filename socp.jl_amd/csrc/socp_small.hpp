@@ -407,31 +407,61 @@ struct Small {
   __device__ __forceinline__ void load_problem(int64_t p) {
     LANE_IDS();
     const double* Gp = a.G + p * (int64_t)k * n;
-    // padding (row >= k or col >= n) reads element 0 and is zeroed with an
-    // integer mask: no per-element exec mask is materialised
+    // G -> AGPRs.  a_put is an asm statement the scheduler does not move loads
+    // across, so the loads are issued in batches of 16 into VGPRs first (one
+    // HBM round trip per batch, not per element).  Padding (row >= k or
+    // col >= n) reads element 0 and is zeroed with an integer mask.
+    constexpr int GT = NP * NQ, GB = 16;
 #pragma unroll
-    for (int pp = 0; pp < NP; ++pp) {
-      const int row = 4 * pp + g;
+    for (int b0 = 0; b0 < GT; b0 += GB) {
+      uint64_t tmp[GB];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int col = 16 * q + cl;
-        const int ok = (row < k) & (col < n);
-        const int64_t idx = ok ? (int64_t)col * k + row : 0;
-        const uint64_t bits = (uint64_t)__double_as_longlong(Gp[idx]) & (0ull - (uint64_t)ok);
-        a_put(G[pp][q], __longlong_as_double((long long)bits));
+      for (int t = 0; t < GB; ++t) {
+        const int e = b0 + t;
+        if (e < GT) {
+          const int pp = e / NQ, q = e % NQ;
+          const int row = 4 * pp + g, col = 16 * q + cl;
+          const int ok = (row < k) & (col < n);
+          const int64_t idx = ok ? (int64_t)col * k + row : 0;
+          tmp[t] = (uint64_t)__double_as_longlong(Gp[idx]) & (0ull - (uint64_t)ok);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < GB; ++t) {
+        const int e = b0 + t;
+        if (e < GT) a_put(G[e / NQ][e % NQ], __longlong_as_double((long long)tmp[t]));
       }
     }
+    // vectors (n, m <= 64 here, k <= 128), loads first, then the LDS writes
+    const double cv = lane < n ? a.c[p * n + lane] : 0.0;
+    const double bv = lane < m ? a.b[p * m + lane] : 0.0;
+    const double hv0 = lane < k ? a.h[p * k + lane] : 0.0;
+    const double hv1 = lane + 64 < k ? a.h[p * k + 64 + lane] : 0.0;
+    const double* Ap = a.A + p * (int64_t)m * n;
+    const int mn = m * n;
+    constexpr int AB = 8;
+    double av[AB];
+#pragma unroll
+    for (int t = 0; t < AB; ++t) av[t] = (64 * t + lane < mn) ? Ap[64 * t + lane] : 0.0;
     for (int e = lane; e < 16 * KMAX; e += 64) LDS(O_KV + e) = 0.0;
     for (int e = lane; e < SH::O_COL - O_A; e += 64) LDS(O_A + e) = 0.0;
     SYNC();
-    const double* Ap = a.A + p * (int64_t)m * n;
-    for (int e = lane; e < m * n; e += 64) {
-      const int i = e % m, j = e / m;
-      LDS(O_A + i * LDA + j) = Ap[e];
+    if (lane < n) LDS(C_ + lane) = cv;
+    if (lane < m) LDS(B_ + lane) = bv;
+    if (lane < k) LDS(H_ + lane) = hv0;
+    if (lane + 64 < k) LDS(H_ + 64 + lane) = hv1;
+    for (int e0 = 0; e0 < mn; e0 += 64 * AB) {
+#pragma unroll
+      for (int t = 0; t < AB; ++t) {
+        const int e = e0 + 64 * t + lane;
+        if (e < mn) LDS(O_A + (e % m) * LDA + e / m) = av[t];
+      }
+      const int e1 = e0 + 64 * AB;
+      if (e1 < mn) {
+#pragma unroll
+        for (int t = 0; t < AB; ++t) av[t] = (e1 + 64 * t + lane < mn) ? Ap[e1 + 64 * t + lane] : 0.0;
+      }
     }
-    for (int j = lane; j < n; j += 64) LDS(C_ + j) = a.c[p * n + j];
-    for (int i = lane; i < m; i += 64) LDS(B_ + i) = a.b[p * m + i];
-    for (int i = lane; i < k; i += 64) LDS(H_ + i) = a.h[p * k + i];
     SYNC();
   }
 
@@ -943,6 +973,94 @@ struct Small {
       }
   }
 
+  // Broadcast across the four 16-lane rows: every lane gets x from the lane of
+  // row R with the same column index (gfx950 v_permlane32_swap / 16_swap).
+  template <int R>
+  __device__ __forceinline__ static double row_bcast(double x) {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto a32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const unsigned ylo = (R < 2) ? a32[0] : a32[1], yhi = (R < 2) ? b32[0] : b32[1];
+    const auto a16 = __builtin_amdgcn_permlane16_swap(ylo, ylo, false, false);
+    const auto b16 = __builtin_amdgcn_permlane16_swap(yhi, yhi, false, false);
+    const unsigned zlo = (R & 1) ? a16[1] : a16[0], zhi = (R & 1) ? b16[1] : b16[0];
+    return __hiloint2double((int)zhi, (int)zlo);
+  }
+
+  // All four row broadcasts of x at once: out[R] = x of row R, same column index.
+  __device__ __forceinline__ static void row_bcast4(double x, double (&out)[4]) {
+    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+    const auto a32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const auto a16 = __builtin_amdgcn_permlane16_swap(a32[h], a32[h], false, false);
+      const auto b16 = __builtin_amdgcn_permlane16_swap(b32[h], b32[h], false, false);
+      out[2 * h] = __hiloint2double((int)b16[0], (int)a16[0]);
+      out[2 * h + 1] = __hiloint2double((int)b16[1], (int)a16[1]);
+    }
+  }
+
+  // Single-pivot steps C.. of panel P (pivot c = 16 P + C, row c of the tile is
+  // register pr of the lanes of row pg).  The lanes of row pg publish row c of
+  // the diagonal tile and of every slab tile through LDS; while those reads are
+  // in flight the pivot column arrives by DPP row_newbcast and the pivot by
+  // readlane.  The diagonal tile is kept exactly symmetric: the rank-1 term is
+  // (D_ic D_cj) / d with one product for (i,j) and (j,i), and the pivot row and
+  // column are the same values times 1/d -- so its row c IS its column c, and
+  // the inverse stays a good right-inverse at kappa ~ 1e10.
+  template <int Q, int P, int C>
+  __device__ __forceinline__ bool sweep_steps(d4& D, d4 (&Z)[Q], d4 (&W)[Q], d4& rv, int cnt, int& step) {
+    if constexpr (C < 16) {
+      constexpr int pr = C / 4, pg = C % 4;
+      if (C >= cnt) return true;
+      LANE_IDS();
+      const bool lane_c = cl == C, lane_r = g == pg;
+      const int cb = O_COL + (step & 1) * SH::CB;
+      ++step;
+      if (lane_r) {
+#pragma unroll
+        for (int i = 0; i < Q; ++i) LDS(cb + 16 * i + cl) = (i == P) ? D[pr] : Z[i][pr];
+      }
+      SYNC();
+      double rowv[Q];  // row c of tile i at column cl
+#pragma unroll
+      for (int i = 0; i < Q; ++i) rowv[i] = LDS(cb + 16 * i + cl);
+      double cR[4];  // lane (g, cl): D[g + 4r][c]
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cR[r] = dpp<0x150 + C, 0xF>(D[r]);
+      const double d = readlane_d(cR[pr], 16 * pg);
+      if (!(d > 0.0)) return false;
+      const double rinv = recip(d);
+      {
+        const double rowD = rowv[P], cC = rowD * rinv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double gen = fma(-(cR[r] * rowD), rinv, D[r]);
+          const double scol = cR[r] * rinv;
+          const bool iR = (r == pr) && lane_r;
+          D[r] = (iR && lane_c) ? -rinv : (lane_c ? scol : (iR ? cC : gen));
+        }
+      }
+      rv[pr] = lane_r ? rinv : rv[pr];
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        if (i == P) continue;
+        const double rc = rowv[i];  // M[c][col]
+        const double rs = rc * rinv;
+        W[i][pr] = lane_r ? rc : W[i][pr];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double gen = fma(-cR[r], rs, Z[i][r]);
+          Z[i][r] = (r == pr && lane_r) ? rs : gen;
+        }
+      }
+      return sweep_steps<Q, P, C + 1>(D, Z, W, rv, cnt, step);
+    } else {
+      return true;
+    }
+  }
+
   // Symmetric Gauss-Jordan sweep of the first nact pivots of a symmetric
   // matrix held as lower tiles in C/D layout; leaves -M^-1 there.  Pivot p is
   // the Schur complement = (Cholesky diagonal)^2, so the failure test is the
@@ -952,16 +1070,13 @@ struct Small {
   // panel slab [M_PP | Z] (Z_i = M_Pi, rows P, cols i != P), which they turn
   // into [-M_PP^-1 | M_PP^-1 Z].  The rank-1 updates the single-pivot sweep
   // would apply to every other tile are deferred: at step c the current row c
-  // of Z over sqrt(d_c) is row c of W = L_PP^-1 Z, and M_OO -= W'W is applied
+  // of Z (rc) and 1/d_c are kept, and M_OO -= sum_c rc_c rc_c'/d_c is applied
   // once per panel with MFMA -- the same sum of rank-1 terms (Gram form, as
   // accurate as the unblocked sweep; the explicit -M_PP^-1-based update is not).
-  template <int Q>
+  template <int Q, int P = 0>
   __device__ __forceinline__ bool sweep(d4 (&M)[Q * (Q + 1) / 2], int nact) {
-    LANE_IDS();
-    int step = 0;
-#pragma unroll
-    for (int P = 0; P < Q; ++P) {
-      if (16 * P >= nact) break;
+    if constexpr (P < Q) {
+      if (16 * P >= nact) return true;
       const int cnt = (nact - 16 * P) < 16 ? (nact - 16 * P) : 16;
       d4 Z[Q], W[Q];
 #pragma unroll
@@ -970,72 +1085,30 @@ struct Small {
         if (i < P) Z[i] = M[tri(P, i)];
         if (i > P) Z[i] = transpose(M[tri(i, P)]);
       }
-      d4& D = M[tri(P, P)];
+      d4 rv = (d4){0.0, 0.0, 0.0, 0.0};  // per lane: 1/d of pivot 4s + g (Gram scaling)
+      {
+        // mirror the lower triangle of the pivot tile onto the upper one (the
+        // Gram updates of earlier panels are symmetric only to rounding)
+        d4& D = M[tri(P, P)];
+        const d4 Dt = transpose(D);
+        LANE_IDS();
 #pragma unroll
-      for (int pr = 0; pr < 4; ++pr) {
-        for (int pg = 0; pg < 4; ++pg) {
-          const int c = 4 * pr + pg;
-          if (c >= cnt) break;
-          const int cb = O_COL + (step & 1) * SH::CB;
-          ++step;
-          const bool lane_c = cl == c, lane_r = g == pg;
-          // gather: column c of the diagonal tile, row c of every slab tile
-          if (lane_c) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) LDS(cb + g + 4 * r) = D[r];
-          }
-          if (lane_r) {
-            LDS(cb + 16 + 16 * P + cl) = D[pr];
-#pragma unroll
-            for (int i = 0; i < Q; ++i)
-              if (i != P) LDS(cb + 16 + 16 * i + cl) = Z[i][pr];
-          }
-          SYNC();
-          const double d = uni(LDS(cb + c));
-          if (!(d > 0.0)) return false;
-          const double rinv = recip(d);
-          const double isd = recip(sqrt(d));
-          double cR[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) cR[r] = LDS(cb + g + 4 * r);
-          // diagonal tile: pivot row and column both from the gathered column
-          // (re-symmetrised every step, which keeps the inverse a good
-          // right-inverse at kappa ~ 1e10)
-          {
-            const double cC = LDS(cb + cl) * rinv;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const double gen = fma(-cR[r], cC, D[r]);
-              const double scol = cR[r] * rinv;
-              const bool iR = (r == pr) && lane_r;
-              D[r] = (iR && lane_c) ? -rinv : (lane_c ? scol : (iR ? cC : gen));
-            }
-          }
-#pragma unroll
-          for (int i = 0; i < Q; ++i) {
-            if (i == P) continue;
-            const double rc = LDS(cb + 16 + 16 * i + cl);  // M[c][col]
-            const double rs = rc * rinv;
-            if (lane_r) W[i][pr] = rc * isd;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const double gen = fma(-cR[r], rs, Z[i][r]);
-              Z[i][r] = (r == pr && lane_r) ? rs : gen;
-            }
-          }
-        }
+        for (int r = 0; r < 4; ++r) D[r] = (g + 4 * r >= cl) ? D[r] : Dt[r];
       }
-      // M_OO -= W'W (lower tiles of every other block row/column)
+      int step = 0;
+      if (!sweep_steps<Q, P, 0>(M[tri(P, P)], Z, W, rv, cnt, step)) return false;
+      // M_OO -= sum_c rc_c rc_c' / d_c (lower tiles of every other block row /
+      // column); lane (g, cl) of k-step s holds pivot 4s + g
 #pragma unroll
       for (int i = 0; i < Q; ++i) {
         if (i == P) continue;
         d4 Wn;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Wn[r] = -W[i][r];
+        for (int r = 0; r < 4; ++r) Wn[r] = -W[i][r] * rv[r];
 #pragma unroll
         for (int j = i; j < Q; ++j) {
           if (j == P) continue;
-          // tile (j, i), j >= i: += W_j' (-W_i)
+          // tile (j, i), j >= i: += W_j' (-W_i / d)
           d4 acc = M[tri(j, i)];
 #pragma unroll
           for (int s = 0; s < 4; ++s) acc = mfma(W[j][s], Wn[s], acc);
@@ -1047,8 +1120,10 @@ struct Small {
         if (i < P) M[tri(P, i)] = Z[i];
         if (i > P) M[tri(i, P)] = transpose(Z[i]);
       }
+      return sweep<Q, P + 1>(M, nact);
+    } else {
+      return true;
     }
-    return true;
   }
 
   __device__ __forceinline__ d4 transpose(d4 t) {
