@@ -77,7 +77,8 @@ enum : int {
   O_CC = O_CKIND + NCS,        // per-cone constants of the current scaling [NCC][NCS]
   O_PART = O_CC + 12 * NCS,    // segment partials [NVMAX][NCS][2 slots] (zero where unused)
   O_TOTC = O_PART + 4 * NCS * 2,  // per-cone results [2][NCS]
-  O_KV = O_TOTC + 2 * NCS,     // 16 k-vectors of KMAX
+  O_STAMPS = O_TOTC + 2 * NCS,  // diagnostic build: per-phase cycle totals of this wave [16]
+  O_KV = O_STAMPS + 16,        // 16 k-vectors of KMAX
   O_FIXED_END = O_KV + 16 * KMAX
 };
 // per-cone constants (SOC cones), recomputed by every scaling:
@@ -122,9 +123,13 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
 // deltas accumulated per problem and added to a global table by lane 0.
 #ifdef SOCP_DIAG
 #define NSTAMP 12
-#define STAMP_DECL uint64_t st_last = 0; uint64_t st_acc[NSTAMP] = {0};
+// Totals live in LDS (lane 0 read-modify-writes them), so the stamps cost no
+// registers beyond the last timestamp; they are flushed once per wave.
+#define STAMP_DECL uint64_t st_last = 0;
 #define STAMP_START_S(obj) do { __builtin_amdgcn_s_waitcnt(0); (obj).st_last = __builtin_amdgcn_s_memtime(); } while (0)
-#define STAMP(i) do { __builtin_amdgcn_s_waitcnt(0); const uint64_t t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_last; st_last = t_; } while (0)
+#define STAMP(i) do { __builtin_amdgcn_s_waitcnt(0); const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0) reinterpret_cast<unsigned long long*>(socp_lds + O_STAMPS)[i] += t_ - st_last; \
+    st_last = t_; } while (0)
 #else
 #define STAMP_DECL
 #define STAMP_START_S(obj) do {} while (0)
@@ -199,6 +204,13 @@ __device__ __forceinline__ double dpp(double v) {
   const int h2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, 0xF, false);
   return __hiloint2double(h2, l2);
 }
+// DPP move whose pattern writes every lane (row_newbcast): no old value needed.
+template <int CTRL>
+__device__ __forceinline__ double dpp_all(double v) {
+  const int l2 = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int h2 = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(h2, l2);
+}
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
@@ -217,6 +229,28 @@ __device__ __forceinline__ int lane_fresh() {
   const int lane = lane_fresh();        \
   const int g = lane >> 4, cl = lane & 15; \
   (void)g; (void)cl
+
+// Sum over the four 16-lane rows (lanes l, l^16, l^32, l^48) with the gfx950
+// row-swap permutes: every lane gets the same total, no LDS round trip.
+__device__ __forceinline__ double rows_sum(double x) {
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const double y = __hiloint2double((int)b[0], (int)a[0]) + __hiloint2double((int)b[1], (int)a[1]);
+  const unsigned ylo = (unsigned)__double2loint(y), yhi = (unsigned)__double2hiint(y);
+  const auto c = __builtin_amdgcn_permlane16_swap(ylo, ylo, false, false);
+  const auto d = __builtin_amdgcn_permlane16_swap(yhi, yhi, false, false);
+  return __hiloint2double((int)d[0], (int)c[0]) + __hiloint2double((int)d[1], (int)c[1]);
+}
+
+// Butterfly partner inside a 16-lane row for reduce-scatter level M, by DPP:
+// M=8 row_ror:8 (l^8), M=4 row_half_mirror (l^7: flips bit 2 like l^4, so the
+// halving is the same), M=2 quad_perm[2,3,0,1] (l^2), M=1 quad_perm[1,0,3,2].
+template <int M>
+__device__ __forceinline__ double row_partner(double v) {
+  constexpr int CTRL = M == 8 ? 0x128 : (M == 4 ? 0x141 : (M == 2 ? 0x4E : 0xB1));
+  return dpp_all<CTRL>(v);
+}
 
 // Wave-uniform copies.  LLVM's divergence analysis treats every LDS or global
 // load as divergent; a branch on such a value (the sweep's pivot test, the
@@ -298,13 +332,13 @@ __device__ __forceinline__ void rs16(double* P, int cl, int& base) {
     for (int j = 0; j < H; ++j) {
       double mine = hi ? P[H + j] : P[j];
       double other = hi ? P[j] : P[H + j];
-      P[j] = mine + __shfl_xor(other, M);
+      P[j] = mine + row_partner<M>(other);
     }
     if (hi) base += H;
     rs16<H, M / 2>(P, cl, base);
   } else {
 #pragma unroll
-    for (int j = 0; j < C; ++j) P[j] += __shfl_xor(P[j], M);
+    for (int j = 0; j < C; ++j) P[j] += row_partner<M>(P[j]);
     rs16<C, M / 2>(P, cl, base);
   }
 }
@@ -384,6 +418,7 @@ struct Small {
     // segment partials: entry (v, c, slot) is written only when cone c meets the
     // slot, the same for every problem of the launch; the rest stays zero
     for (int e = lane; e < O_TOTC - O_PART; e += 64) LDS(O_PART + e) = 0.0;
+    if (lane < 16) LDS(O_STAMPS + lane) = 0.0;  // all-zero bits: the u64 totals start at 0
     SYNC();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -917,8 +952,7 @@ struct Small {
       }
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        acc[q] += __shfl_xor(acc[q], 16);
-        acc[q] += __shfl_xor(acc[q], 32);
+        acc[q] = rows_sum(acc[q]);
       }
       if (g == 0) {
         const double inv = LDS(cc(CC_I1, c));
@@ -1010,10 +1044,11 @@ struct Small {
   // column are the same values times 1/d -- so its row c IS its column c, and
   // the inverse stays a good right-inverse at kappa ~ 1e10.
   template <int Q, int P, int C>
-  __device__ __forceinline__ bool sweep_steps(d4& D, d4 (&Z)[Q], d4 (&W)[Q], d4& rv, int cnt, int& step) {
+  __device__ __forceinline__ void sweep_steps(d4& D, d4 (&Z)[Q], d4 (&W)[Q], d4& rv, int cnt, int& step,
+                                              bool& ok) {
     if constexpr (C < 16) {
       constexpr int pr = C / 4, pg = C % 4;
-      if (C >= cnt) return true;
+      if (C >= cnt) return;
       LANE_IDS();
       const bool lane_c = cl == C, lane_r = g == pg;
       const int cb = O_COL + (step & 1) * SH::CB;
@@ -1028,9 +1063,9 @@ struct Small {
       for (int i = 0; i < Q; ++i) rowv[i] = LDS(cb + 16 * i + cl);
       double cR[4];  // lane (g, cl): D[g + 4r][c]
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cR[r] = dpp<0x150 + C, 0xF>(D[r]);
+      for (int r = 0; r < 4; ++r) cR[r] = dpp_all<0x150 + C>(D[r]);
       const double d = readlane_d(cR[pr], 16 * pg);
-      if (!(d > 0.0)) return false;
+      ok = ok && (d > 0.0);  // a failed pivot poisons the rest; tested once at the end
       const double rinv = recip(d);
       {
         const double rowD = rowv[P], cC = rowD * rinv;
@@ -1055,9 +1090,8 @@ struct Small {
           Z[i][r] = (r == pr && lane_r) ? rs : gen;
         }
       }
-      return sweep_steps<Q, P, C + 1>(D, Z, W, rv, cnt, step);
-    } else {
-      return true;
+      SCHED_FENCE();  // no hoisting of the next step's loads/broadcasts across
+      sweep_steps<Q, P, C + 1>(D, Z, W, rv, cnt, step, ok);
     }
   }
 
@@ -1096,7 +1130,9 @@ struct Small {
         for (int r = 0; r < 4; ++r) D[r] = (g + 4 * r >= cl) ? D[r] : Dt[r];
       }
       int step = 0;
-      if (!sweep_steps<Q, P, 0>(M[tri(P, P)], Z, W, rv, cnt, step)) return false;
+      bool ok = true;
+      sweep_steps<Q, P, 0>(M[tri(P, P)], Z, W, rv, cnt, step, ok);
+      if (!ok) return false;
       // M_OO -= sum_c rc_c rc_c' / d_c (lower tiles of every other block row /
       // column); lane (g, cl) of k-step s holds pivot 4s + g
 #pragma unroll
@@ -1288,8 +1324,7 @@ struct Small {
     }
 #pragma unroll
     for (int t = 0; t < Q; ++t) {
-      P2[t] += __shfl_xor(P2[t], 16);
-      P2[t] += __shfl_xor(P2[t], 32);
+      P2[t] = rows_sum(P2[t]);
     }
     SYNC();
     {
@@ -1360,8 +1395,7 @@ struct Small {
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      acc[q] += __shfl_xor(acc[q], 16);
-      acc[q] += __shfl_xor(acc[q], 32);
+      acc[q] = rows_sum(acc[q]);
     }
   }
 
@@ -1379,8 +1413,7 @@ struct Small {
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      acc[q] += __shfl_xor(acc[q], 16);
-      acc[q] += __shfl_xor(acc[q], 32);
+      acc[q] = rows_sum(acc[q]);
     }
   }
   // out[i] = (A u)[i] - sub[i] for i < m (columns split over the 4 lane groups);
@@ -1394,8 +1427,7 @@ struct Small {
       double acc = 0.0;
 #pragma unroll
       for (int t = 0; t < NQ * 4; ++t) acc = fma(LDS(O_A + i * LDA + g + 4 * t), LDS(u + g + 4 * t), acc);
-      acc += __shfl_xor(acc, 16);
-      acc += __shfl_xor(acc, 32);
+      acc = rows_sum(acc);
       if (g == 0 && i < m) {
         const double v = acc - LDS(sub + i);
         LDS(out + i) = v;
@@ -1698,11 +1730,17 @@ struct Small {
     SYNC();
     STAMP(SP_STORE);
 #ifdef SOCP_DIAG
+    if (lane == 0) reinterpret_cast<unsigned long long*>(socp_lds + O_STAMPS)[NSTAMP] += iters;
+#endif
+  }
+
+  __device__ __forceinline__ void flush_stamps() {
+#ifdef SOCP_DIAG
+    SYNC();
     if (lane == 0 && a.stamps) {
-      for (int i = 0; i < NSTAMP; ++i) atomicAdd(a.stamps + i, (unsigned long long)st_acc[i]);
-      atomicAdd(a.stamps + NSTAMP, (unsigned long long)iters);
+      const unsigned long long* st = reinterpret_cast<const unsigned long long*>(socp_lds + O_STAMPS);
+      for (int i = 0; i <= NSTAMP; ++i) atomicAdd(a.stamps + i, st[i]);
     }
-    for (int i = 0; i < NSTAMP; ++i) st_acc[i] = 0;
 #endif
   }
 };
@@ -1720,6 +1758,7 @@ __global__ void __launch_bounds__(64, 1) socp_small_kernel(SmallArgs args) {
     S.load_problem(p);
     S.run(p);
   }
+  S.flush_stamps();
 }
 
 }  // namespace socp
