@@ -43,12 +43,26 @@ def bytes_per_problem_iter(n, m, k):
     return 8 * (k * n + m * n) + 8 * (n + m + k) + 16 * (n + m + 2 * k)
 
 
+def cone_str(cones):
+    """((kind, offs, dim), ...) -> e.g. 'POC32+SOC32+SOC32' or '8xSOC80'."""
+    parts = [("POC" if kind == 0 else "SOC") + str(dim) for kind, _, dim in cones]
+    out, i = [], 0
+    while i < len(parts):
+        j = i
+        while j < len(parts) and parts[j] == parts[i]:
+            j += 1
+        out.append(parts[i] if j - i == 1 else f"{j - i}x{parts[i]}")
+        i = j
+    return "+".join(out)
+
+
 def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None):
     """Oracle (the reference algorithm restated in C, oracle/) on host cores."""
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle as O  # test infrastructure: timed as the baseline, never the product
     threads = threads or min(16, os.cpu_count() or 1)
-    chunk = 256
+    # one batch of a few seconds: 256 problems at C1/C2, one per thread at C4
+    chunk = 256 if flops_per_problem_iter(cfg.n, cfg.m, cfg.k) < 1e7 else threads
     d = O.generate(cfg.cones, chunk, cfg.n, cfg.m, cfg.k, cfg.seed)
     P = O.Params(maxit=fixed_k, tol=0.0)
     sing = [0] * chunk
@@ -64,7 +78,7 @@ def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None):
             break
     dt = time.perf_counter() - t0
     return {"value": iters / dt, "unit": "problem-iterations/s", "cores": threads, "kind": "port",
-            "sample": f"{reps}x{chunk} C2 problems (first {chunk} of the seeded workload), fixed-K={fixed_k}, "
+            "sample": f"{reps}x{chunk} {cfg.name} problems (first {chunk} of the seeded workload), fixed-K={fixed_k}, "
                       f"oracle/socp_oracle.c (reference op order incl. dense iW*iW' and potrs(I) inverse), "
                       f"OpenMP {threads} threads, {dt:.1f}s"}
 
@@ -102,7 +116,7 @@ def main():
     n, m, k = cfg.n, cfg.m, cfg.k
     ctx = S.Context(local)
     c, A, b, G, h = S.generate(cfg.cones, B, n, m, k, cfg.seed, first_problem=rank * B, ctx=ctx)
-    sing = torch.zeros(B, dtype=torch.uint8, device=dev)  # G (96x64 uniform) has full column rank
+    sing = torch.zeros(B, dtype=torch.uint8, device=dev)  # uniform G (k > n) has full column rank
     ctx.sync()
     out = None
     gathered = torch.empty((world, B, 2), dtype=torch.int32, device=dev) if world > 1 else None
@@ -170,7 +184,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (device SplitMix64 generator, SURVEY.md §8(d); feasible by construction)",
             "config": {
-                "workload": f"{cfg.name}: {B} problems per GPU, n={n}, m={m}, k={k}, cones POC32+SOC32+SOC32, "
+                "workload": f"{cfg.name}: {B} problems per GPU, n={n}, m={m}, k={k}, cones {cone_str(cfg.cones)}, "
                             f"initial point + fixed-K={K} IPM iterations (tol=0)",
                 "global_batch": B * world,
                 "parallelism": f"dp{world} (disjoint problem shards, status all-gather only)",

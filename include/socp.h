@@ -78,6 +78,7 @@ typedef struct socp_params {
 
 #define SOCP_F_DEVICE_PTRS 1 /* all data pointers are device (HBM) pointers */
 #define SOCP_F_WARM_START 2  /* x,y,z,s hold the starting iterate: skip the init solve (solver.jl:68-104) */
+#define SOCP_F_FORCE_LARGE 4 /* run the blocked kernel even where the register-resident one applies (testing, tuning) */
 
 typedef struct socp_ctx socp_ctx;
 
@@ -92,8 +93,11 @@ int socp_ctx_sync(socp_ctx* ctx);
 /* hipStream_t of the context (as void*) so callers can order their own work. */
 void* socp_ctx_stream(socp_ctx* ctx);
 
-/* Largest (n, m, k) the register-resident kernel accepts; other shapes return
- * SOCP_E_UNSUPPORTED from socp_batch_solve. */
+/* 1 if a compiled kernel accepts the dims: the register-resident kernel
+ * (n, m <= 64, k <= 128, <= 8 cones; one wavefront per problem) or the blocked
+ * kernel (n, m <= 512, <= 64 cones, the problem's vectors within the 160 KiB LDS
+ * of a CU -- C4, n=512 m=64 k=640, uses 126 KiB; one 512-thread workgroup per
+ * problem).  Other shapes return SOCP_E_UNSUPPORTED from the solve entries. */
 int socp_supported(const socp_dims* dims);
 
 /* Batched solve: replaces solve_socp(prob, SolverState(prob, DenseSolver(prob)))
@@ -142,7 +146,7 @@ int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims,
                          const double* s, const double* z,
                          const double* dx, const double* dy, const double* dz, const double* ds,
                          double* cx, double* cy, double* cz, double* cs,
-                         int32_t* kkt_status, int32_t flags);
+                         int32_t* kkt_status, int32_t flags);  /* flags: SOCP_F_DEVICE_PTRS | SOCP_F_FORCE_LARGE */
 
 /* Device-side deterministic generator of feasible synthetic problems
  * (SURVEY.md §8(d)): counter-based SplitMix64 keyed on the GLOBAL problem

@@ -57,7 +57,7 @@ struct socp_ctx {
   float last_ms = 0.f;
   const char* last_name = "";
   enum { B_C, B_A, B_B, B_G, B_H, B_SING, B_X, B_Y, B_Z, B_S, B_IT, B_ST, B_RES, B_DX, B_DY,
-         B_DZ, B_DS, B_CX, B_CY, B_CZ, B_CS, B_CNT, NB };
+         B_DZ, B_DS, B_CX, B_CY, B_CZ, B_CS, B_CNT, B_LWS, NB };
   DevBuf buf[NB];
 };
 
@@ -172,10 +172,26 @@ static const SmallVariant* pick_variant(int n, int m, int k) {
   return best;
 }
 
+// The blocked kernel (socp_large.hip): n, m <= 512 (a swept panel row is held
+// in registers) and the problem's vectors within the 160 KiB LDS of a CU.
+static bool large_fits(int n, int m, int k, int nc, size_t* lds_bytes) {
+  const LargeLayout L = large_layout(n, m, k);
+  if (L.NPAD > 64 * LARGE_NB_MAX || L.MPAD > 64 * LARGE_NB_MAX || nc > MAXC) return false;
+  const size_t lds = (size_t)L.total * sizeof(double);
+  if (lds + 64 > 160 * 1024) return false;
+  if (lds_bytes) *lds_bytes = lds;
+  return true;
+}
+
 extern "C" int socp_supported(const socp_dims* d) {
   if (!d) return 0;
-  return pick_variant(d->n, d->m, d->k) != nullptr && d->ncones <= NCS;
+  if (pick_variant(d->n, d->m, d->k) != nullptr && d->ncones <= NCS) return 1;
+  return large_fits(d->n, d->m, d->k, d->ncones, nullptr) ? 1 : 0;
 }
+
+static const char* kUnsupported =
+    "dims outside both kernels (register-resident: n, m <= 64, k <= 128, <= 8 cones; "
+    "blocked: n, m <= 512, <= 64 cones, k-vectors within the 160 KiB LDS)";
 
 // ---------------------------------------------------------------- launch
 static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_DIAG builds)
@@ -198,6 +214,34 @@ static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
   HIPCHK(hipLaunchKernel(v->kernel, dim3((unsigned)blocks), dim3(64), kargs, lds, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
   ctx->last_name = v->name;
+  return 0;
+}
+
+static int launch_large(socp_ctx* ctx, const SmallArgs& a) {
+  size_t lds = 0;
+  if (!large_fits(a.n, a.m, a.k, a.nc, &lds)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
+  const void* kern = large_kernel_ptr();
+  HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int per_cu = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 512, lds));
+  if (per_cu < 1) return fail(SOCP_E_UNSUPPORTED, "blocked kernel does not fit on a CU");
+  int64_t grid = (int64_t)ctx->num_cu * per_cu;
+  if (grid > a.B) grid = a.B;
+  if (grid < 1) grid = 1;
+  const LargeLayout L = large_layout(a.n, a.m, a.k);
+  LargeArgs la;
+  la.a = a;
+  la.a.stamps = g_stamps;
+  la.wstride = L.w_total;
+  const int rc = ctx->buf[socp_ctx::B_LWS].ensure((size_t)grid * (size_t)L.w_total * sizeof(double));
+  if (rc) return fail(rc, "workspace allocation failed");
+  la.ws = (double*)ctx->buf[socp_ctx::B_LWS].p;
+  HIPCHK(hipMemsetAsync(a.counter, 0, sizeof(int32_t), ctx->stream));
+  void* kargs[] = {&la};
+  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIPCHK(hipLaunchKernel(kern, dim3((unsigned)grid), dim3(512), kargs, lds, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  ctx->last_name = large_kernel_name();
   return 0;
 }
 
@@ -269,9 +313,9 @@ extern "C" int socp_batch_solve_ex(socp_ctx* ctx, const socp_dims* dims, const i
   if (B == 0) return 0;
   if (!c || !G || !h || !x || !z || !s || !iters || !status || (m > 0 && (!A || !b || !y)))
     return fail(SOCP_E_INVALID, "NULL data pointer");
-  const SmallVariant* v = pick_variant(n, m, k);
-  if (!v || dims->ncones > NCS)
-    return fail(SOCP_E_UNSUPPORTED, "dims outside the register-resident kernel (n<=64, m<=64, k<=128, <=8 cones)");
+  const bool force_large = (P.flags & SOCP_F_FORCE_LARGE) != 0;
+  const SmallVariant* v = (force_large || dims->ncones > NCS) ? nullptr : pick_variant(n, m, k);
+  if (!v && !large_fits(n, m, k, dims->ncones, nullptr)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
   HIPCHK(hipSetDevice(ctx->device));
   const bool dev = (P.flags & SOCP_F_DEVICE_PTRS) != 0;
   const bool warm = (P.flags & SOCP_F_WARM_START) != 0;
@@ -304,7 +348,7 @@ extern "C" int socp_batch_solve_ex(socp_ctx* ctx, const socp_dims* dims, const i
   TRY(stage_out(ctx, X::B_RES, res, (size_t)B * 3, dev, false, &a.res));
   if (ctx->buf[X::B_CNT].ensure(256)) return fail(SOCP_E_NOMEM, "device allocation failed");
   a.counter = (int32_t*)ctx->buf[X::B_CNT].p;
-  TRY(launch_small(ctx, a, v));
+  TRY(v ? launch_small(ctx, a, v) : launch_large(ctx, a));
   TRY(copy_back(ctx, x, a.x, (size_t)B * n, dev));
   TRY(copy_back(ctx, y, a.y, (size_t)B * m, dev));
   TRY(copy_back(ctx, z, a.z, (size_t)B * k, dev));
@@ -364,8 +408,9 @@ extern "C" int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims, const 
   if (!G || !s || !z || !dx || !dz || !ds || !cx || !cz || !cs || !kkt_status ||
       (m > 0 && (!A || !dy || !cy)))
     return fail(SOCP_E_INVALID, "NULL data pointer");
-  const SmallVariant* v = pick_variant(n, m, k);
-  if (!v || dims->ncones > NCS) return fail(SOCP_E_UNSUPPORTED, "dims outside the register-resident kernel");
+  const bool force_large = (flags & SOCP_F_FORCE_LARGE) != 0;
+  const SmallVariant* v = (force_large || dims->ncones > NCS) ? nullptr : pick_variant(n, m, k);
+  if (!v && !large_fits(n, m, k, dims->ncones, nullptr)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
   HIPCHK(hipSetDevice(ctx->device));
   const bool dev = (flags & SOCP_F_DEVICE_PTRS) != 0;
   a.B = B;
@@ -401,7 +446,7 @@ extern "C" int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims, const 
   TRY(stage_out(ctx, X::B_ST, kkt_status, (size_t)B, dev, false, &a.status));
   if (ctx->buf[X::B_CNT].ensure(256)) return fail(SOCP_E_NOMEM, "device allocation failed");
   a.counter = (int32_t*)ctx->buf[X::B_CNT].p;
-  TRY(launch_small(ctx, a, v));
+  TRY(v ? launch_small(ctx, a, v) : launch_large(ctx, a));
   TRY(copy_back(ctx, cx, a.cx, (size_t)B * n, dev));
   TRY(copy_back(ctx, cy, a.cy, (size_t)B * m, dev));
   TRY(copy_back(ctx, cz, a.cz, (size_t)B * k, dev));

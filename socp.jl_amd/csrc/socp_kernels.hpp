@@ -1,5 +1,6 @@
 // socp_kernels.hpp — internal launch interface between socp_api.hip and the
-// kernel instantiations (socp_small_inst.hip).
+// kernels: the register-resident instantiations (gen_inst.py) and the blocked
+// kernel (socp_large.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include "socp_small.hpp"
@@ -14,5 +15,54 @@ struct SmallVariant {
 
 // table of compiled register-resident variants, ordered by (NQ, NP, MQ)
 const SmallVariant* small_variants(int* count);
+
+// ------------------------------------------------------- blocked kernel
+// socp_large.hip: one 512-thread workgroup per problem, the problem's vectors
+// in LDS, its matrices in a per-workgroup slot of an HBM workspace.
+constexpr int LARGE_NB_MAX = 8;  // NPAD, MPAD <= 512: a swept panel row lives in registers
+
+struct LargeLayout {
+  int NPAD, MPAD, KP, RW;  // n, m rounded up to 64, k to 16; RW = max(NPAD, MPAD)
+  // LDS offsets (doubles)
+  int o_rc, o_cc, o_kv, o_nv, o_mv, o_row, o_rv, o_part, o_red, total;
+  // workspace-slot offsets (doubles)
+  int64_t w_x, w_h, w_ap, w_at, w_yp, w_t, w_s, w_total;
+};
+__host__ __device__ inline int64_t large_al(int64_t v) { return (v + 31) / 32 * 32; }
+__host__ __device__ inline LargeLayout large_layout(int n, int m, int k) {
+  LargeLayout L;
+  L.NPAD = (n + 63) / 64 * 64;
+  L.MPAD = ((m > 0 ? m : 1) + 63) / 64 * 64;
+  L.KP = (k + 15) / 16 * 16;
+  L.RW = L.NPAD > L.MPAD ? L.NPAD : L.MPAD;
+  int o = 0;
+  L.o_rc = o;   o += L.KP;          // element code: cone*4 + type
+  L.o_cc = o;   o += 12 * MAXC;     // per-cone constants CC_*
+  L.o_kv = o;   o += 15 * L.KP;     // k-vectors
+  L.o_nv = o;   o += 6 * L.NPAD;    // n-vectors
+  L.o_mv = o;   o += 5 * L.MPAD;    // m-vectors
+  L.o_row = o;  o += 2 * L.RW;      // sweep pivot-row buffers
+  L.o_rv = o;   o += 64;            // sweep: -1/d of the panel's pivots
+  L.o_part = o; o += 8 * L.MPAD;    // A x partial sums per wavefront
+  L.o_red = o;  o += 64;            // block reductions
+  L.total = o;
+  int64_t w = 0;
+  L.w_x = w;  w += large_al((int64_t)L.KP * L.NPAD);    // X = W^-1 G
+  L.w_h = w;  w += large_al((int64_t)L.NPAD * L.NPAD);  // H -> Li
+  L.w_ap = w; w += large_al((int64_t)L.MPAD * L.NPAD);  // A, column-major
+  L.w_at = w; w += large_al((int64_t)L.NPAD * L.MPAD);  // A, row-major
+  L.w_yp = w; w += large_al((int64_t)64 * L.RW);        // sweep pivot rows
+  L.w_t = w;  w += large_al((int64_t)L.NPAD * L.MPAD);  // Li A'
+  L.w_s = w;  w += large_al((int64_t)L.MPAD * L.MPAD);  // S -> S^-1
+  L.w_total = w;
+  return L;
+}
+struct LargeArgs {
+  SmallArgs a;
+  double* ws;       // grid * wstride doubles
+  int64_t wstride;  // doubles per workspace slot
+};
+const void* large_kernel_ptr();
+const char* large_kernel_name();
 
 }  // namespace socp

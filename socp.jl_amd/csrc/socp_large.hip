@@ -1,0 +1,1076 @@
+// socp_large.hip — the blocked batched dense SOCP IPM kernel (gfx950) for the
+// shapes beyond the register-resident kernel: n and m up to 512, k as LDS
+// allows.  BASELINE config C4 (n=512, m=64, k=640, 8 SOC(80) cones) runs here.
+//
+// One 512-thread workgroup (8 wavefronts) owns one problem for its whole solve;
+// persistent workgroups pull problem indices from an atomic counter.  The
+// problem's vectors live in LDS (C4: 126 KiB), its matrices in the workgroup's
+// slot of an HBM workspace, all column-major:
+//   Xw = W^-1 G (KP x NPAD), rebuilt from G at every factorisation;
+//   Hm = H -> -H^-1 (sweep, lower triangle) -> Li = H^-1 (both triangles);
+//   Ap, At = A zero-padded, column- and row-major;  Tm = Li A' (NPAD x MPAD);
+//   Sm = S -> S^-1;  Yp = the sweep's captured pivot rows (64 x max(NPAD, MPAD)).
+// Per iteration (solver.jl:105-151) the algebra of the register kernel:
+//   H = X'X (+A'A) as f64-MFMA 64x64 blocks: the reference's iWiW GEMM and
+//     G'*iWiW*G products (scalings.jl:108, densesolver.jl:42-46) structurally;
+//   Li = H^-1 by a blocked symmetric Gauss-Jordan sweep (densesolver.jl:47-48):
+//     each 64-pivot row panel is swept in registers (a thread holds 8 panel
+//     rows x NPAD/64 columns; the pivots are the Cholesky pivots, so the
+//     positive-definiteness test is cholesky!'s), and the rank-64 update of
+//     the other blocks is deferred into one MFMA Gram product per panel;
+//   T = Li A', S = A T and S^-1 by the same sweep (densesolver.jl:49-51);
+//   the two KKT solves (densesolver.jl:54-90) as mat-vecs over the workspace.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "socp_kernels.hpp"
+
+namespace socp {
+namespace lg {
+
+constexpr int NW = 8;              // wavefronts per workgroup
+constexpr int NTH = 64 * NW;       // threads per workgroup
+constexpr int NBT = LARGE_NB_MAX;  // 64-column blocks a swept panel row may span
+constexpr int CG = 8;              // columns per wavefront pass in the G' / W^-1 G passes
+constexpr int NOPAD = 1 << 30;     // store_blk: no identity padding
+
+extern __shared__ double lg_lds[];
+#define LV(i) lg_lds[(i)]
+// Workgroup barrier.  Global stores read by other wavefronts after it (the
+// workspace) are drained first; all waves of the workgroup share the CU's L1.
+#define BAR()                                       \
+  do {                                              \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    __syncthreads();                                \
+  } while (0)
+
+// wave-uniform sum / max: DPP inclusive scan to lane 63, broadcast by readlane
+__device__ __forceinline__ double wave_sum(double v) {
+  double x[1] = {v};
+  dpp_scan<1>(x, (int)(threadIdx.x & 63), 0, false);
+  return readlane_d(x[0], 63);
+}
+__device__ __forceinline__ double wave_max(double v) {
+  double x[1] = {v};
+  dpp_scan<1>(x, (int)(threadIdx.x & 63), 0, true);
+  return readlane_d(x[0], 63);
+}
+
+struct Large {
+  const SmallArgs& a;
+  const LargeLayout L;
+  const int n, m, k, nc, tid, lane, wv;
+  int kpoc, csoc;  // POC elements (POC cones come first) and index of the first SOC cone
+  bool sing;
+  const double* Gp;
+  double *Xw, *Hm, *Ap, *At, *Yp, *Tm, *Sm;
+  // LDS vector offsets (doubles)
+  int H_, Z_, S_, DZ, DS, RZ, RS, LAM, WB, CA, K0, K1, K2, T1, T2;
+  int C_, X_, RD, RX, N0, TN;
+  int B_, Y_, RP, RY, M0;
+
+  __device__ Large(const LargeArgs& la)
+      : a(la.a), L(large_layout(la.a.n, la.a.m, la.a.k)), n(la.a.n), m(la.a.m), k(la.a.k),
+        nc(la.a.nc), tid(threadIdx.x), lane(threadIdx.x & 63), wv(threadIdx.x >> 6) {
+    double* ws = la.ws + (int64_t)blockIdx.x * la.wstride;
+    Xw = ws + L.w_x;
+    Hm = ws + L.w_h;
+    Ap = ws + L.w_ap;
+    At = ws + L.w_at;
+    Yp = ws + L.w_yp;
+    Tm = ws + L.w_t;
+    Sm = ws + L.w_s;
+    const int kv = L.o_kv, KP = L.KP;
+    H_ = kv;
+    Z_ = kv + KP;
+    S_ = kv + 2 * KP;
+    DZ = kv + 3 * KP;
+    DS = kv + 4 * KP;
+    RZ = kv + 5 * KP;
+    RS = kv + 6 * KP;
+    LAM = kv + 7 * KP;
+    WB = kv + 8 * KP;
+    CA = kv + 9 * KP;
+    K0 = kv + 10 * KP;
+    K1 = kv + 11 * KP;
+    K2 = kv + 12 * KP;
+    T1 = kv + 13 * KP;
+    T2 = kv + 14 * KP;
+    const int nv = L.o_nv, NP = L.NPAD;
+    C_ = nv;
+    X_ = nv + NP;
+    RD = nv + 2 * NP;
+    RX = nv + 3 * NP;
+    N0 = nv + 4 * NP;
+    TN = nv + 5 * NP;
+    const int mv = L.o_mv, MP = L.MPAD;
+    B_ = mv;
+    Y_ = mv + MP;
+    RP = mv + 2 * MP;
+    RY = mv + 3 * MP;
+    M0 = mv + 4 * MP;
+    kpoc = 0;
+    csoc = 0;
+    for (int c = 0; c < nc && a.cones.kind[c] == POC_K; ++c) {
+      kpoc += a.cones.dim[c];
+      csoc = c + 1;
+    }
+    sing = false;
+    Gp = a.G;
+  }
+
+  __device__ __forceinline__ double ccv(int q, int c) const { return LV(L.o_cc + q * MAXC + c); }
+  __device__ __forceinline__ void ccset(int q, int c, double v) { LV(L.o_cc + q * MAXC + c) = v; }
+  __device__ __forceinline__ double e_of(int i) const {
+    const int t = (int)LV(L.o_rc + i) & 3;
+    return (t == 0 || t == 1) ? 1.0 : 0.0;
+  }
+
+  __device__ double block_sum(double v) {
+    v = wave_sum(v);
+    BAR();
+    if (lane == 0) LV(L.o_red + wv) = v;
+    BAR();
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += LV(L.o_red + w);
+    return t;
+  }
+  __device__ double block_max(double v) {
+    v = wave_max(v);
+    BAR();
+    if (lane == 0) LV(L.o_red + wv) = v;
+    BAR();
+    double t = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t = fmax(t, LV(L.o_red + w));
+    return t;
+  }
+  __device__ bool block_any(bool v) { return block_max(v ? 1.0 : 0.0) > 0.0; }
+
+  // ---------------------------------------------------------------- setup
+  __device__ void init_tables() {
+    for (int i = tid; i < L.KP; i += NTH) {
+      int code = 3;
+      if (i < k)
+        for (int c = 0; c < nc; ++c) {
+          const int o = a.cones.offs[c], d = a.cones.dim[c];
+          if (i >= o && i < o + d) {
+            code = c * 4 + (a.cones.kind[c] == POC_K ? 0 : (i == o ? 1 : 2));
+            break;
+          }
+        }
+      LV(L.o_rc + i) = (double)code;
+    }
+    BAR();
+  }
+
+  __device__ void load(int64_t p) {
+    Gp = a.G + p * (int64_t)k * n;
+    for (int e = tid; e < 15 * L.KP + 6 * L.NPAD + 5 * L.MPAD; e += NTH) LV(L.o_kv + e) = 0.0;
+    BAR();
+    for (int j = tid; j < n; j += NTH) LV(C_ + j) = a.c[p * n + j];
+    for (int i = tid; i < m; i += NTH) LV(B_ + i) = a.b[p * m + i];
+    for (int i = tid; i < k; i += NTH) LV(H_ + i) = a.h[p * k + i];
+    const double* Ag = a.A + p * (int64_t)m * n;
+    const int NP = L.NPAD, MP = L.MPAD;
+    for (int e = tid; e < MP * NP; e += NTH) {
+      const int j = e / MP, r = e - j * MP;
+      double v = 0.0;
+      if (r < m && j < n) v = Ag[(int64_t)j * m + r];
+      Ap[e] = v;
+    }
+    for (int e = tid; e < MP * NP; e += NTH) {
+      const int r = e / NP, j = e - r * NP;
+      double v = 0.0;
+      if (r < m && j < n) v = Ag[(int64_t)j * m + r];
+      At[e] = v;
+    }
+    BAR();
+  }
+
+  // W = I: the initial-point system (solver.jl:68-84) is the KKT system with
+  // W = I, lambda = e, ds = 0.
+  __device__ void scaling_identity() {
+    for (int i = tid; i < k; i += NTH) {
+      const double e = e_of(i);
+      LV(WB + i) = e;
+      LV(LAM + i) = e;
+      LV(CA + i) = 1.0;
+    }
+    for (int c = tid; c < nc; c += NTH) {
+      ccset(CC_MU, c, 1.0);
+      ccset(CC_IMU, c, 1.0);
+      ccset(CC_WB0, c, 1.0);
+      ccset(CC_I1, c, 0.5);
+      ccset(CC_W2, c, 0.0);
+      ccset(CC_L0, c, 1.0);
+      ccset(CC_AA, c, 1.0);
+      ccset(CC_IAA, c, 1.0);
+      ccset(CC_IL0, c, 1.0);
+      ccset(CC_IL0AA, c, 1.0);
+      ccset(CC_SA, c, 1.0);
+      ccset(CC_SAL, c, 0.5);
+    }
+    BAR();
+  }
+
+  // ------------------------------------------------------ cone vector ops
+  // POC elements are elementwise over all threads; SOC cone c belongs to
+  // wavefront (c - csoc) % 8, whose lanes stride over the cone's elements and
+  // reduce its dot products with wave_sum.  Formulas: the register kernel's.
+
+  // compute_scaling (scalings.jl:22-110) and ds = lam o lam (solver.jl:120)
+  __device__ bool scaling_op(double& ll, bool& dm_aa, bool write_ds) {
+    double llp = 0.0;
+    bool dm = false, da = false;
+    for (int i = tid; i < kpoc; i += NTH) {
+      const double s = LV(S_ + i), z = LV(Z_ + i);
+      const double r = s / z, pr = s * z, ir = z / s;
+      dm |= (r < 0.0) || (pr < 0.0) || (ir < 0.0);
+      const double li = sqrt(pr);
+      LV(WB + i) = sqrt(r);
+      LV(LAM + i) = li;
+      LV(CA + i) = sqrt(ir);
+      if (write_ds) LV(DS + i) = li * li;
+      llp += li * li;
+    }
+    for (int c = csoc + wv; c < nc; c += NW) {
+      const int o = a.cones.offs[c], d = a.cones.dim[c];
+      const double z0 = LV(Z_ + o), s0 = LV(S_ + o);
+      double pz = 0.0, ps = 0.0, pzs = 0.0;
+      for (int i = o + 1 + lane; i < o + d; i += 64) {
+        const double zi = LV(Z_ + i), si = LV(S_ + i);
+        pz += zi * zi;
+        ps += si * si;
+        pzs += zi * si;
+      }
+      const double vz = wave_sum(pz), vs = wave_sum(ps), vzs = wave_sum(pzs);
+      const double onrmz = z0 * z0 - vz, onrms = s0 * s0 - vs;
+      const double nrmz = sqrt(onrmz), nrms = sqrt(onrms);
+      const double fz = 1.0 / nrmz, fs = 1.0 / nrms;
+      const double zb0 = z0 * fz, sb0 = s0 * fs;
+      const double nsum = zb0 * sb0 + vzs * fz * fs;
+      const double garg = (1.0 + nsum) / 2.0;
+      const double gamma = sqrt(garg);
+      const double fg = 1.0 / (2.0 * gamma);
+      const double wb0 = (sb0 + zb0) * fg;
+      const double ratio = nrms / nrmz, prod = nrms * nrmz;
+      const double mu = sqrt(ratio), tmv1 = sqrt(prod);
+      const double mult = tmv1 / (zb0 + sb0 + 2.0 * gamma);
+      const double l0 = gamma * tmv1;
+      const double im = 1.0 / mu;
+      dm |= (onrmz < 0.0) || (onrms < 0.0) || (garg < 0.0) || (ratio < 0.0) || (prod < 0.0);
+      double pl = 0.0, pw = 0.0;
+      for (int i = o + 1 + lane; i < o + d; i += 64) {
+        const double zbi = LV(Z_ + i) * fz, sbi = LV(S_ + i) * fs;
+        const double w = (sbi - zbi) * fg;
+        const double li = (sbi * (gamma + zb0) + zbi * (gamma + sb0)) * mult;
+        LV(WB + i) = w;
+        LV(LAM + i) = li;
+        if (write_ds) LV(DS + i) = l0 * li + l0 * li;
+        pl += li * li;
+        pw += w * w;
+      }
+      const double v1 = wave_sum(pl), v2 = wave_sum(pw);
+      const double v0 = l0 * l0 + v1;  // lam'lam of the cone (vprod!'s head, vectors.jl:66)
+      const double aa = l0 * l0 - v1;  // iprod!'s a (vectors.jl:105)
+      da |= aa < 0.0;
+      if (lane == 0) {
+        LV(WB + o) = wb0;
+        LV(LAM + o) = l0;
+        if (write_ds) LV(DS + o) = v0;
+        const double sa = 1.0 / sqrt(aa);
+        ccset(CC_MU, c, mu);
+        ccset(CC_IMU, c, im);
+        ccset(CC_WB0, c, wb0);
+        ccset(CC_I1, c, 1.0 / (1.0 + wb0));
+        ccset(CC_W2, c, v2);
+        ccset(CC_L0, c, l0);
+        ccset(CC_AA, c, aa);
+        ccset(CC_IAA, c, 1.0 / aa);
+        ccset(CC_IL0, c, 1.0 / l0);
+        ccset(CC_IL0AA, c, 1.0 / (l0 * aa));
+        ccset(CC_SA, c, sa);
+        ccset(CC_SAL, c, 1.0 / (sa * l0 + 1.0));
+        llp += v0;
+      }
+    }
+    ll = block_sum(llp);
+    dm_aa = block_any(da);
+    return block_any(dm);
+  }
+
+  // First half of solve_kkt (densesolver.jl:61-66): k0 = lam^-1 o ds, k1 = W k0,
+  // k2 = dz - k1, T2 = W^-1 W^-1 k2.  In: DS, DZ.  Out: K0, K2, T2.
+  __device__ void solve_head() {
+    for (int i = tid; i < kpoc; i += NTH) {
+      const double k0 = LV(DS + i) / LV(LAM + i);
+      const double k2 = LV(DZ + i) - LV(WB + i) * k0;
+      const double ca = LV(CA + i);
+      LV(K0 + i) = k0;
+      LV(K2 + i) = k2;
+      LV(T2 + i) = ca * (ca * k2);
+    }
+    for (int c = csoc + wv; c < nc; c += NW) {
+      const int o = a.cones.offs[c], d = a.cones.dim[c];
+      const double x0 = LV(DS + o);
+      double pt = 0.0;
+      for (int i = o + 1 + lane; i < o + d; i += 64) pt = fma(LV(LAM + i), LV(DS + i), pt);
+      const double t = wave_sum(pt);
+      const double l0 = ccv(CC_L0, c), iaa = ccv(CC_IAA, c), il0 = ccv(CC_IL0, c), il0aa = ccv(CC_IL0AA, c);
+      const double k00 = (x0 * l0 - t) * iaa;
+      double pd = 0.0;
+      for (int i = o + 1 + lane; i < o + d; i += 64) {
+        const double lam = LV(LAM + i);
+        const double k0 = -(x0 * lam * iaa) + LV(DS + i) * il0 + lam * t * il0aa;
+        LV(K0 + i) = k0;
+        pd = fma(LV(WB + i), k0, pd);
+      }
+      const double del = wave_sum(pd);
+      const double mu = ccv(CC_MU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
+      const double k10 = mu * (wb0 * k00 + del);
+      const double k20 = LV(DZ + o) - k10;
+      double pa = 0.0;
+      for (int i = o + 1 + lane; i < o + d; i += 64) {
+        const double wb = LV(WB + i);
+        const double k2 = LV(DZ + i) - mu * (LV(K0 + i) + (k00 + del * i1) * wb);
+        LV(K2 + i) = k2;
+        pa = fma(wb, k2, pa);
+      }
+      const double a1 = wave_sum(pa);
+      const double im = ccv(CC_IMU, c), w2 = ccv(CC_W2, c);
+      const double cy = a1 * i1 - k20;
+      const double y0 = im * (wb0 * k20 - a1);
+      const double a2 = im * (a1 + cy * w2);
+      for (int i = o + 1 + lane; i < o + d; i += 64) {
+        const double wb = LV(WB + i);
+        const double y = im * (LV(K2 + i) + cy * wb);
+        LV(T2 + i) = im * (y + (a2 * i1 - y0) * wb);
+      }
+      if (lane == 0) {
+        LV(K0 + o) = k00;
+        LV(K2 + o) = k20;
+        LV(T2 + o) = im * (wb0 * y0 - a2);
+      }
+    }
+    BAR();
+  }
+
+  // Second half of solve_kkt (densesolver.jl:83-88) and, with do_step,
+  // compute_step (mats.jl:30-86) of the direction: kt3 = W rz (T1) and
+  // kt2 = W^-1 rs (K0) come out of the solve.  In: K1, K0.  Out: RZ, RS, T1, K0.
+  __device__ double solve_tail(bool do_step, bool dm_aa, int& dom) {
+    double mx = -INFINITY;
+    for (int i = tid; i < kpoc; i += NTH) {
+      const double ca = LV(CA + i), y = ca * LV(K1 + i);
+      const double kn = LV(K0 + i) - y;
+      LV(RZ + i) = ca * y;
+      LV(RS + i) = LV(WB + i) * kn;
+      LV(T1 + i) = y;
+      LV(K0 + i) = kn;
+      const double lam = LV(LAM + i);
+      mx = fmax(mx, fmax(-y / lam, -kn / lam));
+    }
+    for (int c = csoc + wv; c < nc; c += NW) {
+      const int o = a.cones.offs[c], d = a.cones.dim[c];
+      const double k10 = LV(K1 + o);
+      double p1 = 0.0;
+      for (int i = o + 1 + lane; i < o + d; i += 64) p1 = fma(LV(WB + i), LV(K1 + i), p1);
+      const double a1 = wave_sum(p1);
+      const double im = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c), w2 = ccv(CC_W2, c);
+      const double mu = ccv(CC_MU, c);
+      const double cy = a1 * i1 - k10;
+      const double y0 = im * (wb0 * k10 - a1);
+      const double a2 = im * (a1 + cy * w2);
+      const double kn0 = LV(K0 + o) - y0;
+      double pd = 0.0;
+      for (int i = o + 1 + lane; i < o + d; i += 64) {
+        const double wb = LV(WB + i);
+        const double y = im * (LV(K1 + i) + cy * wb);
+        const double kn = LV(K0 + i) - y;
+        LV(RZ + i) = im * (y + (a2 * i1 - y0) * wb);
+        LV(T1 + i) = y;
+        LV(K0 + i) = kn;
+        pd = fma(wb, kn, pd);
+      }
+      const double del = wave_sum(pd);
+      for (int i = o + 1 + lane; i < o + d; i += 64)
+        LV(RS + i) = mu * (LV(K0 + i) + (kn0 + del * i1) * LV(WB + i));
+      if (lane == 0) {
+        LV(RZ + o) = im * (wb0 * y0 - a2);
+        LV(RS + o) = mu * (wb0 * kn0 + del);
+        LV(T1 + o) = y0;
+        LV(K0 + o) = kn0;
+      }
+      if (do_step) {  // scmax (mats.jl:42-86) of kt3 and kt2
+        double pw0 = 0.0, pw1 = 0.0;
+        for (int i = o + 1 + lane; i < o + d; i += 64) {
+          const double lam = LV(LAM + i);
+          pw0 = fma(lam, LV(T1 + i), pw0);
+          pw1 = fma(lam, LV(K0 + i), pw1);
+        }
+        const double w0 = wave_sum(pw0), w1 = wave_sum(pw1);
+        const double sa = ccv(CC_SA, c), l0 = ccv(CC_L0, c), sal = ccv(CC_SAL, c);
+        const double r1y = sa * l0 * y0 - sa * w0, r1k = sa * l0 * kn0 - sa * w1;
+        const double cyy = (r1y + y0) * sal, cyk = (r1k + kn0) * sal;
+        double qy = 0.0, qk = 0.0;
+        for (int i = o + 1 + lane; i < o + d; i += 64) {
+          const double lam = LV(LAM + i);
+          const double ty = sa * (LV(T1 + i) - cyy * sa * lam), tk = sa * (LV(K0 + i) - cyk * sa * lam);
+          qy = fma(ty, ty, qy);
+          qk = fma(tk, tk, qk);
+        }
+        const double vy = sqrt(wave_sum(qy)) - sa * r1y, vk = sqrt(wave_sum(qk)) - sa * r1k;
+        mx = fmax(mx, fmax(vy, vk));
+      }
+    }
+    if (!do_step) {
+      BAR();
+      return 0.0;
+    }
+    const double t = fmax(block_max(mx), 0.0);
+    dom = dm_aa ? 1 : 0;
+    return (t == 0.0) ? 1.0 : fmin(1.0, 1.0 / t);
+  }
+
+  // rho, sigma, mu (solver.jl:132-134) and the corrector right-hand side
+  // (:136-140).  In: K0 (kt2), T1 (kt3), DS, DZ, RD, RP.
+  __device__ void affine_post(double tstep, double ll) {
+    double pk = 0.0;
+    for (int i = tid; i < k; i += NTH) pk = fma(LV(K0 + i), LV(T1 + i), pk);
+    const double kk = block_sum(pk);
+    const double t = tstep;
+    const double rho = 1.0 - t - t * t * kk / ll;
+    const double cr = isnan(rho) ? rho : (rho < 0.0 ? 0.0 : (rho > 1.0 ? 1.0 : rho));
+    const double sig = ipow(cr, a.sigma_exp);  // max(0,min(1,rho))^3 (solver.jl:133)
+    const double mu_ipm = ll / a.deg;
+    const double scf = 1.0 - sig;
+    for (int i = tid; i < kpoc; i += NTH) LV(DS + i) = LV(DS + i) + (sig * mu_ipm - LV(K0 + i) * LV(T1 + i));
+    for (int c = csoc + wv; c < nc; c += NW) {
+      const int o = a.cones.offs[c], d = a.cones.dim[c];
+      double ph = 0.0;
+      for (int i = o + lane; i < o + d; i += 64) ph = fma(LV(K0 + i), LV(T1 + i), ph);
+      const double hsum = wave_sum(ph);
+      const double a20 = LV(K0 + o), a30 = LV(T1 + o);
+      for (int i = o + 1 + lane; i < o + d; i += 64)
+        LV(DS + i) = LV(DS + i) - (a20 * LV(T1 + i) + a30 * LV(K0 + i));
+      if (lane == 0) LV(DS + o) = LV(DS + o) + (sig * mu_ipm - hsum);
+    }
+    for (int i = tid; i < k; i += NTH) LV(DZ + i) = LV(DZ + i) * scf;
+    for (int j = tid; j < n; j += NTH) LV(RD + j) = LV(RD + j) * scf;
+    for (int i = tid; i < m; i += NTH) LV(RP + i) = LV(RP + i) * scf;
+    BAR();
+  }
+
+  // max_step(-iz), max_step(iz) (mats.jl:1-28) for the initial shift (solver.jl:88-101)
+  __device__ void maxstep_op(int xv, double& alphp, double& alphd) {
+    double mp = -INFINITY, md = -INFINITY;
+    for (int i = tid; i < kpoc; i += NTH) {
+      const double x = LV(xv + i);
+      mp = fmax(mp, x);
+      md = fmax(md, -x);
+    }
+    for (int c = csoc + wv; c < nc; c += NW) {
+      const int o = a.cones.offs[c], d = a.cones.dim[c];
+      double pq = 0.0;
+      for (int i = o + 1 + lane; i < o + d; i += 64) pq = fma(LV(xv + i), LV(xv + i), pq);
+      const double nr = sqrt(wave_sum(pq)), x0 = LV(xv + o);
+      mp = fmax(mp, nr + x0);
+      md = fmax(md, nr - x0);
+    }
+    alphp = block_max(mp);
+    alphd = block_max(md);
+  }
+
+  // ---------------------------------------------------------- dense blocks
+  // acc[ta][tb] += sum_kk P[kk][I0+16ta+i] * Q[kk][J0+16tb+j] over kk < kr, where
+  // P[kk][col] sits at P[col*ld + kk] (column-major, k index fastest).  At MFMA
+  // step s, lane group g feeds k-row k0 + 4g + s (the k order is free), so a
+  // lane's operands are 4 consecutive doubles (two 16-byte loads).  qs >= 0:
+  // the Q operand of k-row kk is scaled by LDS[qs + kk].
+  __device__ __forceinline__ void blk_gemm(d4 (&acc)[4][4], const double* P, const double* Q, int ld, int I0,
+                                           int J0, int kr, bool same, int qs) {
+    const int g = lane >> 4, cl = lane & 15;
+    for (int k0 = 0; k0 < kr; k0 += 16) {
+      double av[4][4], bv[4][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const double2* pa = reinterpret_cast<const double2*>(P + (int64_t)(I0 + 16 * t + cl) * ld + k0 + 4 * g);
+        const double2 x0 = pa[0], x1 = pa[1];
+        av[t][0] = x0.x;
+        av[t][1] = x0.y;
+        av[t][2] = x1.x;
+        av[t][3] = x1.y;
+      }
+      if (same) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) bv[t][s] = av[t][s];
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const double2* pb = reinterpret_cast<const double2*>(Q + (int64_t)(J0 + 16 * t + cl) * ld + k0 + 4 * g);
+          const double2 x0 = pb[0], x1 = pb[1];
+          bv[t][0] = x0.x;
+          bv[t][1] = x0.y;
+          bv[t][2] = x1.x;
+          bv[t][3] = x1.y;
+        }
+      }
+      if (qs >= 0) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const double f = LV(qs + k0 + 4 * g + s);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) bv[t][s] *= f;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+          for (int tb = 0; tb < 4; ++tb) acc[ta][tb] = mfma(av[ta][s], bv[tb][s], acc[ta][tb]);
+    }
+  }
+
+  // 64x64 block (I0, J0) of a column-major matrix <-> the f64 MFMA C/D layout
+  // (lane (g, cl) holds rows g + 4r, column cl of each 16x16 tile)
+  __device__ __forceinline__ void load_blk(d4 (&acc)[4][4], const double* M, int ld, int I0, int J0) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[ta][tb][r] = M[(int64_t)(J0 + 16 * tb + cl) * ld + I0 + 16 * ta + g + 4 * r];
+  }
+  // idpad: diagonal entries at index >= idpad are set to 1 (identity padding)
+  __device__ __forceinline__ void store_blk(const d4 (&acc)[4][4], double* M, int ld, int I0, int J0, int idpad) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int R = I0 + 16 * ta + g + 4 * r, Cc = J0 + 16 * tb + cl;
+          const double v = (R == Cc && R >= idpad) ? 1.0 : acc[ta][tb][r];
+          M[(int64_t)Cc * ld + R] = v;
+        }
+  }
+  __device__ __forceinline__ static void zero_blk(d4 (&acc)[4][4]) {
+#pragma unroll
+    for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb) acc[ta][tb] = (d4){0.0, 0.0, 0.0, 0.0};
+  }
+  // lower-triangle block index t -> (I, J), I >= J
+  __device__ __forceinline__ static void tri_ij(int t, int& I, int& J) {
+    I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    J = t - I * (I + 1) / 2;
+  }
+
+  // X[:, j] = W^-1 G[:, j] (iscale!, scalings.jl:145-173) for every column:
+  // a wavefront takes CG columns at a time (independent per-cone reductions
+  // overlap).  Zero padding (rows >= k, columns >= n).
+  __device__ void form_X() {
+    const int KP = L.KP;
+    for (int j0 = CG * wv; j0 < L.NPAD; j0 += CG * NW) {
+      const double* gc[CG];
+      double* xc[CG];
+      bool live[CG];
+#pragma unroll
+      for (int u = 0; u < CG; ++u) {
+        const int j = j0 + u;
+        live[u] = j < n;
+        gc[u] = Gp + (int64_t)(live[u] ? j : 0) * k;
+        xc[u] = Xw + (int64_t)j * KP;
+      }
+      for (int i = lane; i < kpoc; i += 64) {
+        const double ca = LV(CA + i);
+#pragma unroll
+        for (int u = 0; u < CG; ++u) xc[u][i] = live[u] ? ca * gc[u][i] : 0.0;
+      }
+      for (int c = csoc; c < nc; ++c) {
+        const int o = a.cones.offs[c], d = a.cones.dim[c];
+        double pd[CG];
+#pragma unroll
+        for (int u = 0; u < CG; ++u) pd[u] = 0.0;
+        for (int i = o + 1 + lane; i < o + d; i += 64) {
+          const double wb = LV(WB + i);
+#pragma unroll
+          for (int u = 0; u < CG; ++u) pd[u] = fma(wb, gc[u][i], pd[u]);
+        }
+        const double im = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
+        double cst[CG];
+#pragma unroll
+        for (int u = 0; u < CG; ++u) {
+          const double del = wave_sum(pd[u]);
+          const double g0 = gc[u][o];
+          cst[u] = -g0 + del * i1;
+          if (lane == 0) xc[u][o] = live[u] ? im * (wb0 * g0 - del) : 0.0;
+        }
+        for (int i = o + 1 + lane; i < o + d; i += 64) {
+          const double wb = LV(WB + i);
+#pragma unroll
+          for (int u = 0; u < CG; ++u) xc[u][i] = live[u] ? im * (gc[u][i] + cst[u] * wb) : 0.0;
+        }
+      }
+      for (int i = k + lane; i < KP; i += 64) {
+#pragma unroll
+        for (int u = 0; u < CG; ++u) xc[u][i] = 0.0;
+      }
+    }
+    BAR();
+  }
+
+  // H = X'X (+A'A) (densesolver.jl:42-46): lower 64x64 blocks, one wavefront
+  // per block; padding diagonal = 1.
+  __device__ void form_H(bool addAA) {
+    const int NB = L.NPAD / 64, nblk = NB * (NB + 1) / 2;
+    for (int t = wv; t < nblk; t += NW) {
+      int I, J;
+      tri_ij(t, I, J);
+      d4 acc[4][4];
+      zero_blk(acc);
+      blk_gemm(acc, Xw, Xw, L.KP, 64 * I, 64 * J, L.KP, I == J, -1);
+      if (addAA) blk_gemm(acc, Ap, Ap, L.MPAD, 64 * I, 64 * J, L.MPAD, I == J, -1);
+      store_blk(acc, Hm, L.NPAD, 64 * I, 64 * J, n);
+    }
+    BAR();
+  }
+
+  // Blocked symmetric Gauss-Jordan sweep of the 64nb x 64nb symmetric matrix
+  // whose lower triangle is stored in M (column-major, ld); leaves -M^-1 in the
+  // lower triangle.  Panel P: thread (wave w, lane l) holds panel rows
+  // 64P + w + 8q (q < 8) at columns 64t + l; at step c the owner of row c
+  // publishes it through LDS (the pivot column is the same row by symmetry,
+  // which the update keeps exact: one product per (i,j)/(j,i) pair) and records
+  // it in Yp.  Pivot d = the Schur complement = (Cholesky diagonal)^2, so the
+  // failure test is the one LAPACK potrf applies (d <= 0 or NaN).  The other
+  // blocks get M_IJ -= sum_c rc_c[I]' rc_c[J] / d_c once per panel (MFMA).
+  __device__ bool sweep(double* M, int ld, int nb) {
+    const int rr = wv;
+    for (int P = 0; P < nb; ++P) {
+      const int P0 = 64 * P;
+      double Z[8][NBT];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int x = P0 + rr + 8 * q;
+#pragma unroll
+        for (int t = 0; t < NBT; ++t) {
+          Z[q][t] = 0.0;
+          if (t < nb) {
+            const int y = 64 * t + lane;
+            Z[q][t] = (y <= x) ? M[(int64_t)y * ld + x] : M[(int64_t)x * ld + y];
+          }
+        }
+      }
+      bool ok = true;
+      for (int c = 0; c < 64; ++c) {
+        const int buf = L.o_row + (c & 1) * L.RW;
+        if (wv == (c & 7)) {
+          const int qc = c >> 3;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            if (q == qc) {
+#pragma unroll
+              for (int t = 0; t < NBT; ++t)
+                if (t < nb) {
+                  LV(buf + 64 * t + lane) = Z[q][t];
+                  Yp[(int64_t)(64 * t + lane) * 64 + c] = Z[q][t];
+                }
+            }
+          }
+        }
+        __syncthreads();
+        const double d = LV(buf + P0 + c);
+        ok = ok && (d > 0.0);
+        const double r = 1.0 / d;
+        if (tid == 0) LV(L.o_rv + c) = -r;
+        double rowv[NBT], colv[8];
+#pragma unroll
+        for (int t = 0; t < NBT; ++t) rowv[t] = (t < nb) ? LV(buf + 64 * t + lane) : 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) colv[q] = LV(buf + P0 + rr + 8 * q);
+        const int p = P0 + c;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const bool xr = (rr + 8 * q) == c;
+#pragma unroll
+          for (int t = 0; t < NBT; ++t) {
+            if (t < nb) {
+              const bool yc = (64 * t + lane) == p;
+              const double gen = fma(-(colv[q] * rowv[t]), r, Z[q][t]);
+              Z[q][t] = (xr && yc) ? -r : (yc ? colv[q] * r : (xr ? rowv[t] * r : gen));
+            }
+          }
+        }
+      }
+      BAR();  // Yp and the pivot reciprocals complete
+      if (!ok) return false;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int x = P0 + rr + 8 * q;
+#pragma unroll
+        for (int t = 0; t < NBT; ++t)
+          if (t < nb) {
+            const int y = 64 * t + lane;
+            if (y <= x)
+              M[(int64_t)y * ld + x] = Z[q][t];
+            else
+              M[(int64_t)x * ld + y] = Z[q][t];
+          }
+      }
+      const int no = nb - 1, ng = no * (no + 1) / 2;
+      for (int t = wv; t < ng; t += NW) {
+        int a_, b_;
+        tri_ij(t, a_, b_);
+        const int I = a_ + (a_ >= P ? 1 : 0), J = b_ + (b_ >= P ? 1 : 0);
+        d4 acc[4][4];
+        load_blk(acc, M, ld, 64 * I, 64 * J);
+        blk_gemm(acc, Yp, Yp, 64, 64 * I, 64 * J, 64, false, L.o_rv);
+        store_blk(acc, M, ld, 64 * I, 64 * J, NOPAD);
+      }
+      BAR();
+    }
+    return true;
+  }
+
+  // M (lower triangle = -X^-1) -> X^-1 in both triangles
+  __device__ void finalize_sym(double* M, int ld) {
+    const int64_t tot = (int64_t)ld * ld;
+    for (int64_t e = tid; e < tot; e += NTH) {
+      const int C = (int)(e / ld), R = (int)(e - (int64_t)C * ld);
+      if (R >= C) {
+        const double v = -M[e];
+        M[e] = v;
+        if (R != C) M[(int64_t)R * ld + C] = v;
+      }
+    }
+    BAR();
+  }
+
+  // setup_iter (densesolver.jl:41-52): H (+A'A), Li = H^-1, T = Li A', S = A T, S^-1
+  __device__ int factor(bool addAA, bool h_only) {
+    form_X();
+    form_H(addAA);
+    if (!sweep(Hm, L.NPAD, L.NPAD / 64)) return ST_CHOL_H;
+    if (h_only) return 0;
+    finalize_sym(Hm, L.NPAD);
+    const int NB = L.NPAD / 64, MB = L.MPAD / 64;
+    for (int t = wv; t < NB * MB; t += NW) {
+      const int I = t / MB, J = t - I * MB;
+      d4 acc[4][4];
+      zero_blk(acc);
+      blk_gemm(acc, Hm, At, L.NPAD, 64 * I, 64 * J, L.NPAD, false, -1);
+      store_blk(acc, Tm, L.NPAD, 64 * I, 64 * J, NOPAD);
+    }
+    BAR();
+    for (int t = wv; t < MB * (MB + 1) / 2; t += NW) {
+      int I, J;
+      tri_ij(t, I, J);
+      d4 acc[4][4];
+      zero_blk(acc);
+      blk_gemm(acc, At, Tm, L.NPAD, 64 * I, 64 * J, L.NPAD, false, -1);
+      store_blk(acc, Sm, L.MPAD, 64 * I, 64 * J, m);
+    }
+    BAR();
+    if (!sweep(Sm, L.MPAD, MB)) return ST_CHOL_S;
+    finalize_sym(Sm, L.MPAD);
+    return 0;
+  }
+
+  // ------------------------------------------------------------ mat-vecs
+  // out[j] = (G' vin)[j] (+ add[j]) for j < n: a wavefront takes CG columns
+  __device__ void gemv_Gt(int vin, int vout, int vadd) {
+    for (int j0 = CG * wv; j0 < n; j0 += CG * NW) {
+      const double* gc[CG];
+      double acc[CG];
+#pragma unroll
+      for (int u = 0; u < CG; ++u) {
+        gc[u] = Gp + (int64_t)(j0 + u < n ? j0 + u : n - 1) * k;
+        acc[u] = 0.0;
+      }
+      for (int i = lane; i < k; i += 64) {
+        const double v = LV(vin + i);
+#pragma unroll
+        for (int u = 0; u < CG; ++u) acc[u] = fma(gc[u][i], v, acc[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < CG; ++u) {
+        const double s = wave_sum(acc[u]);
+        if (lane == 0 && j0 + u < n) LV(vout + j0 + u) = (vadd >= 0) ? s + LV(vadd + j0 + u) : s;
+      }
+    }
+    BAR();
+  }
+  // out[i] = (G u)[i] (+ add[i]) - sub[i] for i < k: one thread per row
+  __device__ void gemv_G(int u, int add, int sub, int out) {
+    for (int i = tid; i < k; i += NTH) {
+      double acc = 0.0;
+#pragma unroll 16
+      for (int j = 0; j < n; ++j) acc = fma(Gp[(int64_t)j * k + i], LV(u + j), acc);
+      if (add >= 0) acc = acc + LV(add + i);
+      LV(out + i) = acc - LV(sub + i);
+    }
+    BAR();
+  }
+  // (A' v)[j] for one j (thread per column; At rows are contiguous in j)
+  __device__ __forceinline__ double At_dot(int v, int j) const {
+    double acc = 0.0;
+    for (int r = 0; r < m; ++r) acc = fma(At[(int64_t)r * L.NPAD + j], LV(v + r), acc);
+    return acc;
+  }
+  // out[r] = (A u)[r] - sub[r] for r < m; returns this thread's share of |out|^2
+  __device__ double A_mv(int u, int sub, int out) {
+    for (int r = lane; r < L.MPAD; r += 64) {
+      double acc = 0.0;
+      for (int j = wv; j < n; j += NW) acc = fma(Ap[(int64_t)j * L.MPAD + r], LV(u + j), acc);
+      LV(L.o_part + wv * L.MPAD + r) = acc;
+    }
+    BAR();
+    double sq = 0.0;
+    for (int r = tid; r < m; r += NTH) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += LV(L.o_part + w * L.MPAD + r);
+      const double v = s - LV(sub + r);
+      LV(out + r) = v;
+      sq = fma(v, v, sq);
+    }
+    BAR();
+    return sq;
+  }
+  // out = M vin for a full symmetric column-major M (thread per row)
+  __device__ void symv(const double* M, int ld, int vin, int vout) {
+    for (int i = tid; i < ld; i += NTH) {
+      double acc = 0.0;
+#pragma unroll 16
+      for (int j = 0; j < ld; ++j) acc = fma(M[(int64_t)j * ld + i], LV(vin + j), acc);
+      LV(vout + i) = acc;
+    }
+    BAR();
+  }
+
+  // rd = A'y + G'z + c, rp = Ax - b, rz = Gx + s - h (solver.jl:109-118)
+  __device__ void residuals(double& nd, double& np_, double& gap) {
+    gemv_Gt(Z_, TN, -1);
+    double d2 = 0.0;
+    for (int j = tid; j < n; j += NTH) {
+      const double v = (At_dot(Y_, j) + LV(TN + j)) + LV(C_ + j);
+      LV(RD + j) = v;
+      d2 = fma(v, v, d2);
+    }
+    const double p2 = A_mv(X_, B_, RP);
+    gemv_G(X_, S_, H_, DZ);
+    double zs = 0.0;
+    for (int i = tid; i < k; i += NTH) zs += LV(Z_ + i) * LV(S_ + i);
+    nd = sqrt(block_sum(d2));
+    np_ = sqrt(block_sum(p2));
+    gap = block_sum(zs);
+  }
+
+  // The matrix part of solve_kkt (densesolver.jl:66-85): n0 = GWiWi*k2 + dx
+  // (+A'dy if sing); m0 = A Li n0 - dy; cy = S^-1 m0; m0 = sing ? dy - cy : -cy
+  // (init: -cy); n0 += A'm0; cx = Li n0; k1 = G cx - k2.
+  // In: RD RP T2 K2.  Out: RX RY K1.
+  __device__ void solve_matrix_part(bool init) {
+    gemv_Gt(T2, N0, RD);
+    if (sing) {
+      for (int j = tid; j < n; j += NTH) LV(N0 + j) = LV(N0 + j) + At_dot(RP, j);
+      BAR();
+    }
+    symv(Hm, L.NPAD, N0, TN);
+    A_mv(TN, RP, M0);
+    symv(Sm, L.MPAD, M0, RY);
+    for (int r = tid; r < m; r += NTH) LV(M0 + r) = (sing && !init) ? LV(RP + r) - LV(RY + r) : -LV(RY + r);
+    BAR();
+    for (int j = tid; j < n; j += NTH) LV(N0 + j) = LV(N0 + j) + At_dot(M0, j);
+    BAR();
+    symv(Hm, L.NPAD, N0, RX);
+    gemv_G(RX, -1, K2, K1);
+  }
+
+  // ------------------------------------------------------------- driver
+  // solve_socp (solver.jl:40-153) for problem p: the register kernel's control
+  // flow and status rules.
+  __device__ void run(int64_t p) {
+    load(p);
+    int status = ST_MAXIT, iters = 0;
+    double nd = NAN, np_ = NAN, gap = NAN, ll = 0.0;
+    bool dm_aa = false;
+    if (a.sing) {
+      sing = a.sing[p] != 0;
+    } else {  // Problem's `sing` (Socp.jl:49-56): does cholesky(G'G) fail?
+      scaling_identity();
+      sing = factor(false, true) == ST_CHOL_H;
+    }
+    if (a.mode == MODE_KKT) {
+      for (int i = tid; i < k; i += NTH) {
+        LV(S_ + i) = a.s[p * k + i];
+        LV(Z_ + i) = a.z[p * k + i];
+        LV(DZ + i) = a.dz[p * k + i];
+        LV(DS + i) = a.ds[p * k + i];
+      }
+      for (int j = tid; j < n; j += NTH) LV(RD + j) = a.dx[p * n + j];
+      for (int i = tid; i < m; i += NTH) LV(RP + i) = a.dy[p * m + i];
+      BAR();
+      if (scaling_op(ll, dm_aa, false)) {
+        status = ST_DOMAIN;
+      } else {
+        const int f = factor(sing, false);
+        if (f) {
+          status = f;
+        } else {
+          solve_head();
+          solve_matrix_part(false);
+          int dom = 0;
+          solve_tail(false, dm_aa, dom);
+          status = 0;
+          for (int j = tid; j < n; j += NTH) a.cx[p * n + j] = LV(RX + j);
+          for (int i = tid; i < m; i += NTH) a.cy[p * m + i] = LV(RY + i);
+          for (int i = tid; i < k; i += NTH) {
+            a.cz[p * k + i] = LV(RZ + i);
+            a.cs[p * k + i] = LV(RS + i);
+          }
+        }
+      }
+      if (tid == 0) a.status[p] = status;
+      BAR();
+      return;
+    }
+    bool go = true;
+    if (a.flags & F_WARM) {
+      for (int j = tid; j < n; j += NTH) LV(X_ + j) = a.x[p * n + j];
+      for (int i = tid; i < m; i += NTH) LV(Y_ + i) = a.y[p * m + i];
+      for (int i = tid; i < k; i += NTH) {
+        LV(Z_ + i) = a.z[p * k + i];
+        LV(S_ + i) = a.s[p * k + i];
+      }
+      BAR();
+    } else {  // initial point: the KKT system with W = I (solver.jl:68-84), then the shift (:86-104)
+      scaling_identity();
+      for (int j = tid; j < n; j += NTH) LV(RD + j) = -LV(C_ + j);
+      for (int i = tid; i < m; i += NTH) LV(RP + i) = LV(B_ + i);
+      for (int i = tid; i < k; i += NTH) {
+        LV(DZ + i) = LV(H_ + i);
+        LV(DS + i) = 0.0;
+      }
+      BAR();
+      const int f = factor(sing, false);
+      if (f) {
+        status = f;
+        go = false;
+      } else {
+        solve_head();
+        solve_matrix_part(true);
+        int dom = 0;
+        solve_tail(false, false, dom);
+        double alphp, alphd;
+        maxstep_op(RZ, alphp, alphd);
+        for (int j = tid; j < n; j += NTH) LV(X_ + j) = LV(RX + j);
+        for (int i = tid; i < m; i += NTH) LV(Y_ + i) = LV(RY + i);
+        for (int i = tid; i < k; i += NTH) {
+          const double iz = LV(RZ + i), e = e_of(i);
+          LV(S_ + i) = (fabs(alphp) < a.init_eps) ? -iz : -iz + (1.0 + alphp) * e;
+          LV(Z_ + i) = (fabs(alphd) < a.init_eps) ? iz : iz + (1.0 + alphd) * e;
+        }
+        BAR();
+      }
+    }
+    int it = 0;
+    while (go) {
+      residuals(nd, np_, gap);
+      if (it >= a.maxit) break;
+      if (scaling_op(ll, dm_aa, true)) {
+        status = ST_DOMAIN;
+        break;
+      }
+      if (nd + np_ + gap < a.tol) {
+        status = ST_CONVERGED;
+        break;
+      }
+      for (int j = tid; j < n; j += NTH) LV(RD + j) = -LV(RD + j);
+      for (int i = tid; i < m; i += NTH) LV(RP + i) = -LV(RP + i);
+      for (int i = tid; i < k; i += NTH) {
+        LV(DZ + i) = -LV(DZ + i);
+        LV(DS + i) = -LV(DS + i);
+      }
+      BAR();
+      const int f = factor(sing, false);
+      if (f) {
+        status = f;
+        break;
+      }
+      solve_head();  // affine direction (solver.jl:125-130)
+      solve_matrix_part(false);
+      int dom = 0;
+      double t = solve_tail(true, dm_aa, dom);
+      if (dom) {
+        status = ST_DOMAIN;
+        break;
+      }
+      affine_post(t, ll);
+      solve_head();  // combined direction (solver.jl:141-145)
+      solve_matrix_part(false);
+      t = solve_tail(true, dm_aa, dom);
+      if (dom) {
+        status = ST_DOMAIN;
+        break;
+      }
+      const double stp = t * a.step;  // step and update (solver.jl:146-150)
+      for (int j = tid; j < n; j += NTH) LV(X_ + j) = LV(X_ + j) + LV(RX + j) * stp;
+      for (int i = tid; i < m; i += NTH) LV(Y_ + i) = LV(Y_ + i) + LV(RY + i) * stp;
+      for (int i = tid; i < k; i += NTH) {
+        LV(Z_ + i) = LV(Z_ + i) + LV(RZ + i) * stp;
+        LV(S_ + i) = LV(S_ + i) + LV(RS + i) * stp;
+      }
+      BAR();
+      iters = ++it;
+    }
+    for (int j = tid; j < n; j += NTH) a.x[p * n + j] = LV(X_ + j);
+    for (int i = tid; i < m; i += NTH) a.y[p * m + i] = LV(Y_ + i);
+    for (int i = tid; i < k; i += NTH) {
+      a.z[p * k + i] = LV(Z_ + i);
+      a.s[p * k + i] = LV(S_ + i);
+    }
+    if (tid == 0) {
+      if (a.res) {
+        a.res[3 * p + 0] = nd;
+        a.res[3 * p + 1] = np_;
+        a.res[3 * p + 2] = gap;
+      }
+      a.iters[p] = iters;
+      a.status[p] = status;
+    }
+    BAR();
+  }
+};
+
+__global__ void __launch_bounds__(NTH, 1) socp_large_kernel(LargeArgs args) {
+  __shared__ int pidx;
+  Large S(args);
+  S.init_tables();
+  while (true) {
+    if (threadIdx.x == 0) pidx = atomicAdd(args.a.counter, 1);
+    __syncthreads();
+    const int64_t p = pidx;
+    __syncthreads();  // everyone has read pidx before thread 0 overwrites it
+    if (p >= args.a.B) break;
+    S.run(p);
+  }
+}
+
+}  // namespace lg
+
+const void* large_kernel_ptr() { return (const void*)&lg::socp_large_kernel; }
+const char* large_kernel_name() { return "socp_large_kernel"; }
+
+}  // namespace socp

@@ -19,7 +19,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (CHOL_H_FAILED, CHOL_S_FAILED, CONE_POC, CONE_SOC, CONVERGED, DOMAIN_ERROR,
-                   F_DEVICE_PTRS, F_WARM_START, MAXIT, Context, SocpError, default_context,
+                   F_DEVICE_PTRS, F_FORCE_LARGE, F_WARM_START, MAXIT, Context, SocpError, default_context,
                    default_params)
 
 __all__ = [
@@ -97,14 +97,15 @@ def _host(a, dtype=np.float64):
 
 
 def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5, step=0.99,
-                sigma_exp=3, init_eps=1e-10, warm=None, ctx=None, res=False, out=None):
+                sigma_exp=3, init_eps=1e-10, warm=None, ctx=None, res=False, out=None, force_large=False):
     """Solve a batch of independent problems (same dims and cone structure).
 
     Arrays follow include/socp.h: per-problem column-major A (m x n), G (k x n)
     stacked batch-major, vectors stacked batch-major.  numpy inputs run through
     host staging buffers; torch CUDA tensors are used in place (device mode,
     stream-ordered on the context's stream; call ctx.sync() before reading).
-    Returns dict(x, y, z, s, iters, status[, res]).
+    force_large runs the blocked kernel (socp_large.hip) even where the
+    register-resident one applies.  Returns dict(x, y, z, s, iters, status[, res]).
     """
     ctx = ctx or default_context()
     L = _lib.load()
@@ -115,6 +116,8 @@ def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5,
     flags = F_DEVICE_PTRS if dev else 0
     if warm is not None:
         flags |= F_WARM_START
+    if force_large:
+        flags |= F_FORCE_LARGE
     P = default_params(maxit=maxit, tol=tol, step=step, sigma_exp=sigma_exp, init_eps=init_eps,
                        flags=flags)
     if dev:
@@ -158,7 +161,7 @@ def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5,
     return out
 
 
-def batch_kkt_solve(cones, n, m, k, A, G, sing, s, z, dx, dy, dz, ds, *, ctx=None):
+def batch_kkt_solve(cones, n, m, k, A, G, sing, s, z, dx, dy, dz, ds, *, ctx=None, force_large=False):
     """One KKT solve per problem at iterate (s, z): scaling + setup_iter + solve_kkt
     (densesolver.jl:41-90) on the GPU.  Host (numpy) arrays.  Returns dict(cx,cy,cz,cs,status)."""
     ctx = ctx or default_context()
@@ -173,7 +176,8 @@ def batch_kkt_solve(cones, n, m, k, A, G, sing, s, z, dx, dy, dz, ds, *, ctx=Non
     rc = L.socp_batch_kkt_solve(ctx.handle, dims, p(kind), p(offs), p(dim),
                                 p(_host(A) if m else None), p(_host(G)), p(sg), p(_host(s)), p(_host(z)),
                                 p(_host(dx)), p(_host(dy) if m else None), p(_host(dz)), p(_host(ds)),
-                                p(cx), p(cy if m else None), p(cz), p(cs), p(st), 0)
+                                p(cx), p(cy if m else None), p(cz), p(cs), p(st),
+                                F_FORCE_LARGE if force_large else 0)
     _lib.check(rc)
     return dict(cx=cx, cy=cy[:B * m], cz=cz, cs=cs, status=st)
 

@@ -42,10 +42,13 @@ def test_default_params_are_reference_constants():
 
 def test_supported_dims():
     L = _lib.load()
-    for name, ok in (("C0b", True), ("C1", True), ("C2", True), ("C4", False)):
+    for name, ok in (("C0b", True), ("C1", True), ("C2", True), ("C4", True)):
         cfg = CONFIGS[name]
         d = _lib.Dims(cfg.batch, cfg.n, cfg.m, cfg.k, len(cfg.cones))
         assert bool(L.socp_supported(C.byref(d))) == ok, name
+    # beyond the blocked kernel: n > 512, or k-vectors over the 160 KiB LDS
+    for n, m, k, nc in ((600, 0, 601, 1), (512, 64, 1000, 8)):
+        assert not L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
 
 
 def test_null_context_is_an_api_error():

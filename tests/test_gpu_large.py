@@ -1,0 +1,165 @@
+"""Parity of the blocked kernel (socp_large.hip) with the CPU oracle.
+
+The blocked kernel runs the shapes beyond the register-resident kernel
+(n or m > 64, k > 128, > 8 cones), BASELINE config C4 (n=512) among them.
+force_large=True (SOCP_F_FORCE_LARGE) also runs it on the C0b/C1/C2 shapes, so
+it is held to the register kernel's gates (tests/test_gpu_parity.py):
+trajectory rel <= 1e-8 (P4), outcome parity (P5), the KKT golden <= 1e-10
+(P2), the device-side `sing` test, NaN isolation.  Then the shapes only it
+runs: the n=150 optimal-control problem of runtests.jl:204-244 (m=102: S
+spans two sweep panels) and C4 (first iterations vs the oracle at B=2,
+properties of the full 1,024-problem batch).
+"""
+import numpy as np
+import pytest
+
+import socp_amd as S
+from socp_amd.configs import C0B, C1, C2, C4
+from problems import optimal_control
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a).reshape(-1)
+    b = np.asarray(b).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+def run(cfg, d, **kw):
+    return S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                         kw.pop("sing", None), **kw)
+
+
+def oracle_run(oracle, cfg, d, **kw):
+    return oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"], **kw)
+
+
+def assert_trajectory(cfg, g, r, B, tol, tag):
+    assert (g["status"] == r["status"]).all(), (tag, g["status"], r["status"])
+    for p in range(B):
+        for key, L in (("x", cfg.n), ("z", cfg.k), ("s", cfg.k)):
+            e = rel(g[key][p * L:(p + 1) * L], r[key][p * L:(p + 1) * L])
+            assert e <= tol, (tag, p, key, e)
+
+
+@pytest.mark.parametrize("cfg,maxk", [(C1, 3), (C2, 6)])
+def test_forced_large_trajectory(oracle, cfg, maxk):
+    B = 16
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    for K in range(1, maxk + 1):
+        r = oracle_run(oracle, cfg, d, params=oracle.Params(maxit=K, tol=0.0))
+        g = run(cfg, d, maxit=K, tol=0.0, force_large=True)
+        assert_trajectory(cfg, g, r, B, 1e-8, K)
+
+
+def test_forced_large_agrees_with_register_kernel(oracle):
+    # the same algebra blocked two ways: equal to rounding
+    cfg, B = C2, 32
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    a = run(cfg, d, maxit=4, tol=0.0)
+    b = run(cfg, d, maxit=4, tol=0.0, force_large=True)
+    assert (a["status"] == b["status"]).all()
+    for p in range(B):
+        e = rel(b["x"][p * cfg.n:(p + 1) * cfg.n], a["x"][p * cfg.n:(p + 1) * cfg.n])
+        assert e <= 1e-9, (p, e)
+
+
+def test_forced_large_outcome(oracle):
+    cfg, B = C1, 64
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    r = oracle_run(oracle, cfg, d)
+    g = run(cfg, d, res=True, force_large=True)
+    ok = r["status"] == 0
+    assert ok.mean() >= 0.95
+    assert (g["status"][ok] == 0).all()
+    assert np.abs(g["iters"][ok] - r["iters"][ok]).max() <= 1
+    dx = np.abs(g["x"].reshape(B, -1) - r["x"].reshape(B, -1)).max(axis=1)
+    assert dx[ok].max() <= 1e-3
+    res = g["res"].reshape(B, 3)
+    gc = g["status"] == 0
+    assert (res[gc].sum(axis=1) < 1e-5).all()
+
+
+def test_forced_large_sing_c0b(oracle):
+    cfg, B = C0B, 32
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    r = oracle_run(oracle, cfg, d)
+    g = run(cfg, d, force_large=True)  # sing detected on the device
+    ok = r["status"] == 0
+    assert ok.mean() > 0.9
+    assert (g["status"][ok] == 0).all()
+    assert np.abs(g["iters"][ok] - r["iters"][ok]).max() <= 1
+    dx = np.abs(g["x"].reshape(B, -1) - r["x"].reshape(B, -1)).max(axis=1)
+    assert dx[ok].max() <= 1e-3
+
+
+def test_forced_large_kkt_golden(kats):
+    g = kats["kkt_golden"]
+    cones = [tuple(c) for c in g["cones"]]
+    G = np.array(g["G"])
+    out = S.batch_kkt_solve(cones, 3, 0, 4, None, G.ravel(order="F"), None, np.array(g["s"]), np.array(g["z"]),
+                            np.array(g["dx"]), None, np.array(g["dz"]), np.array(g["ds"]), force_large=True)
+    assert out["status"][0] == 0
+    for key in ("cx", "cz", "cs"):
+        assert np.abs(out[key] - np.array(g[key])).max() <= 1e-10, key
+
+
+def test_forced_large_nan_isolation(oracle):
+    cfg, B = C2, 8
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    ref = run(cfg, d, maxit=4, tol=0.0, force_large=True)
+    bad = dict(d)
+    bad["G"] = d["G"].copy()
+    bad["G"][3 * cfg.k * cfg.n + 17] = np.nan
+    got = run(cfg, bad, maxit=4, tol=0.0, force_large=True)
+    assert got["status"][3] in (S.CHOL_H_FAILED, S.CHOL_S_FAILED, S.DOMAIN_ERROR)
+    others = np.arange(B) != 3
+    assert np.array_equal(got["status"][others], ref["status"][others])
+    assert np.array_equal(got["x"].reshape(B, -1)[others], ref["x"].reshape(B, -1)[others])
+
+
+def test_optimal_control_n150(oracle):
+    """runtests.jl:204-244 'linear optimal control': n=150, m=102, k=50, one SOC,
+    G'G singular (`sing`, so H = G'W^-2G + A'A).  Beyond the register kernel."""
+    cones, c, A, b, G, h = optimal_control(50)
+    n, m, k = len(c), A.shape[0], G.shape[0]
+    for K in (1, 2, 3):
+        r = oracle.solve_trace(cones, c, A, b, G, h, params=oracle.Params(maxit=K, tol=0.0))
+        g = S.batch_solve(cones, n, m, k, c, A.ravel(order="F"), b, G.ravel(order="F"), h, None,
+                          maxit=K, tol=0.0)
+        assert g["status"][0] == r["status"], (K, g["status"][0], r["status"])
+        if r["status"] == S.MAXIT:
+            assert rel(g["x"], r["x"]) <= 1e-6, (K, rel(g["x"], r["x"]))
+
+
+def test_c4_trajectory(oracle):
+    """C4 (n=512, m=64, k=640, 8 SOC(80)): first iterations vs the oracle, 2 problems."""
+    cfg, B = C4, 2
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    for K in (1, 2):
+        r = oracle_run(oracle, cfg, d, params=oracle.Params(maxit=K, tol=0.0))
+        g = run(cfg, d, maxit=K, tol=0.0)
+        assert S.default_context().last_kernel_name() == "socp_large_kernel"
+        assert_trajectory(cfg, g, r, B, 1e-8, K)
+
+
+def test_c4_full_batch_properties():
+    """The BASELINE C4 batch (1,024 problems, fixed-K=5, device-resident): every
+    problem runs its 5 iterations and stays strictly inside its 8 cones."""
+    import torch
+    cfg = C4
+    B = cfg.batch
+    c, A, b, G, h = S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    sing = torch.zeros(B, dtype=torch.uint8, device=G.device)
+    out = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=cfg.fixed_k, tol=0.0, res=True)
+    S.default_context().sync()
+    st = out["status"].cpu().numpy()
+    assert (st == S.MAXIT).mean() > 0.99, np.bincount(st)
+    okp = st == S.MAXIT
+    for key in ("z", "s"):
+        arr = out[key].cpu().numpy().reshape(B, cfg.k)
+        for o in range(0, cfg.k, 80):
+            assert (arr[okp, o] > np.linalg.norm(arr[okp, o + 1:o + 80], axis=1)).all(), (key, o)
+    res = out["res"].cpu().numpy().reshape(B, 3)
+    assert np.isfinite(res[okp]).all()

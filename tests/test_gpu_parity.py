@@ -88,12 +88,12 @@ def test_sing_batch_c0b(oracle):
     assert dx[ok].max() <= 1e-3
 
 
-def test_large_n_reports_unsupported():
-    # n = 150 (optimal control, runtests.jl:204) is beyond the register-resident kernel
-    cones, c, A, b, G, h = optimal_control(50)
-    prob = S.Problem(c, A, b, G, h, cones)
+def test_beyond_both_kernels_reports_unsupported():
+    # n = 600 > 512: outside the blocked kernel too (the n=150 runtests.jl problem
+    # and C4 run on the blocked kernel: tests/test_gpu_large.py)
+    n, m, k = 600, 0, 601
     with pytest.raises(S.SocpError) as e:
-        S.solve_socp(prob, S.SolverState(prob, S.DenseSolver(prob)))
+        S.batch_solve([(1, 0, k)], n, m, k, np.zeros(n), None, None, np.zeros(k * n), np.zeros(k))
     assert e.value.code == -2
 
 
