@@ -35,6 +35,14 @@ constexpr int NBT = LARGE_NB_MAX;  // 64-column blocks a swept panel row may spa
 constexpr int CG = 8;              // columns per wavefront pass in the G' / W^-1 G passes
 constexpr int NOPAD = 1 << 30;     // store_blk: no identity padding
 
+// Workspace and problem pointers in the global address space (otherwise, once
+// they pass through the stack object of an out-of-line member call, the
+// compiler sees generic pointers and emits flat instructions).
+typedef __attribute__((address_space(1))) double gdbl;
+typedef __attribute__((address_space(1))) const double gcdbl;
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const dbl2 gcdbl2;
+
 extern __shared__ double lg_lds[];
 #define LV(i) lg_lds[(i)]
 // Workgroup barrier.  Global stores read by other wavefronts after it (the
@@ -44,6 +52,24 @@ extern __shared__ double lg_lds[];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
     __syncthreads();                                \
   } while (0)
+
+// Diagnostic build (-DSOCP_DIAG): thread 0 adds per-phase s_memtime deltas
+// into u64 totals at LDS o_red + 16 (its own timeline: the phases end in
+// workgroup barriers), flushed to args.stamps once per workgroup.
+#ifdef SOCP_DIAG
+#define LSTAMP(i)                                                                          \
+  do {                                                                                     \
+    if (tid == 0) {                                                                        \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();                                    \
+      reinterpret_cast<unsigned long long*>(lg_lds + L.o_red + 16)[(i)] += t_ - st_last;    \
+      st_last = t_;                                                                        \
+    }                                                                                      \
+  } while (0)
+#else
+#define LSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
 
 // wave-uniform sum / max: DPP inclusive scan to lane 63, broadcast by readlane
 __device__ __forceinline__ double wave_sum(double v) {
@@ -63,17 +89,19 @@ struct Large {
   const int n, m, k, nc, tid, lane, wv;
   int kpoc, csoc;  // POC elements (POC cones come first) and index of the first SOC cone
   bool sing;
-  const double* Gp;
-  double *Xw, *Hm, *Ap, *At, *Yp, *Tm, *Sm;
+  gcdbl* Gp;
+  gdbl *Xw, *Hm, *Ap, *At, *Yp, *Tm, *Sm;
   // LDS vector offsets (doubles)
   int H_, Z_, S_, DZ, DS, RZ, RS, LAM, WB, CA, K0, K1, K2, T1, T2;
   int C_, X_, RD, RX, N0, TN;
   int B_, Y_, RP, RY, M0;
+  uint64_t st_last = 0;
 
   __device__ Large(const LargeArgs& la)
       : a(la.a), L(large_layout(la.a.n, la.a.m, la.a.k)), n(la.a.n), m(la.a.m), k(la.a.k),
-        nc(la.a.nc), tid(threadIdx.x), lane(threadIdx.x & 63), wv(threadIdx.x >> 6) {
-    double* ws = la.ws + (int64_t)blockIdx.x * la.wstride;
+        nc(la.a.nc), tid(threadIdx.x), lane(threadIdx.x & 63),
+        wv(__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6)) {
+    gdbl* ws = (gdbl*)la.ws + (int64_t)blockIdx.x * la.wstride;
     Xw = ws + L.w_x;
     Hm = ws + L.w_h;
     Ap = ws + L.w_ap;
@@ -117,7 +145,7 @@ struct Large {
       csoc = c + 1;
     }
     sing = false;
-    Gp = a.G;
+    Gp = (gcdbl*)a.G;
   }
 
   __device__ __forceinline__ double ccv(int q, int c) const { return LV(L.o_cc + q * MAXC + c); }
@@ -163,11 +191,22 @@ struct Large {
         }
       LV(L.o_rc + i) = (double)code;
     }
+    if (tid < 16) LV(L.o_red + 16 + tid) = 0.0;  // all-zero bits: the u64 stamp totals start at 0
     BAR();
+    st_last = __builtin_amdgcn_s_memtime();
+  }
+  __device__ void flush_stamps() {
+#ifdef SOCP_DIAG
+    BAR();
+    if (tid == 0 && a.stamps) {
+      const unsigned long long* st = reinterpret_cast<const unsigned long long*>(lg_lds + L.o_red + 16);
+      for (int i = 0; i <= NSTAMP; ++i) atomicAdd(a.stamps + i, st[i]);
+    }
+#endif
   }
 
   __device__ void load(int64_t p) {
-    Gp = a.G + p * (int64_t)k * n;
+    Gp = (gcdbl*)a.G + p * (int64_t)k * n;
     for (int e = tid; e < 15 * L.KP + 6 * L.NPAD + 5 * L.MPAD; e += NTH) LV(L.o_kv + e) = 0.0;
     BAR();
     for (int j = tid; j < n; j += NTH) LV(C_ + j) = a.c[p * n + j];
@@ -490,15 +529,15 @@ struct Large {
   // step s, lane group g feeds k-row k0 + 4g + s (the k order is free), so a
   // lane's operands are 4 consecutive doubles (two 16-byte loads).  qs >= 0:
   // the Q operand of k-row kk is scaled by LDS[qs + kk].
-  __device__ __forceinline__ void blk_gemm(d4 (&acc)[4][4], const double* P, const double* Q, int ld, int I0,
+  __device__ __forceinline__ void blk_gemm(d4 (&acc)[4][4], gcdbl* P, gcdbl* Q, int ld, int I0,
                                            int J0, int kr, bool same, int qs) {
     const int g = lane >> 4, cl = lane & 15;
     for (int k0 = 0; k0 < kr; k0 += 16) {
       double av[4][4], bv[4][4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const double2* pa = reinterpret_cast<const double2*>(P + (int64_t)(I0 + 16 * t + cl) * ld + k0 + 4 * g);
-        const double2 x0 = pa[0], x1 = pa[1];
+        gcdbl2* pa = reinterpret_cast<gcdbl2*>(P + (int64_t)(I0 + 16 * t + cl) * ld + k0 + 4 * g);
+        const dbl2 x0 = pa[0], x1 = pa[1];
         av[t][0] = x0.x;
         av[t][1] = x0.y;
         av[t][2] = x1.x;
@@ -512,8 +551,8 @@ struct Large {
       } else {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const double2* pb = reinterpret_cast<const double2*>(Q + (int64_t)(J0 + 16 * t + cl) * ld + k0 + 4 * g);
-          const double2 x0 = pb[0], x1 = pb[1];
+          gcdbl2* pb = reinterpret_cast<gcdbl2*>(Q + (int64_t)(J0 + 16 * t + cl) * ld + k0 + 4 * g);
+          const dbl2 x0 = pb[0], x1 = pb[1];
           bv[t][0] = x0.x;
           bv[t][1] = x0.y;
           bv[t][2] = x1.x;
@@ -537,9 +576,36 @@ struct Large {
     }
   }
 
+  // acc[ta][tb] += sum_{c<64} Y[c][I0+16ta+i] * (LDS[qs+c] * Y[c][J0+16tb+j]) for the
+  // row-major 64-row panel Y (row c at Y + c*ld): the sweep's deferred Gram update.
+  // At MFMA step s, lane group g feeds row k0 + 4s + g (C/D row order).
+  __device__ __forceinline__ void gram_blk(d4 (&acc)[4][4], gcdbl* Y, int ld, int I0, int J0, int qs) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll 1
+    for (int k0 = 0; k0 < 64; k0 += 16) {
+      double av[4][4], bv[4][4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        gcdbl* row = Y + (int64_t)(k0 + 4 * s + g) * ld;
+        const double f = LV(qs + k0 + 4 * s + g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          av[t][s] = row[I0 + 16 * t + cl];
+          bv[t][s] = f * row[J0 + 16 * t + cl];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+          for (int tb = 0; tb < 4; ++tb) acc[ta][tb] = mfma(av[ta][s], bv[tb][s], acc[ta][tb]);
+    }
+  }
+
   // 64x64 block (I0, J0) of a column-major matrix <-> the f64 MFMA C/D layout
   // (lane (g, cl) holds rows g + 4r, column cl of each 16x16 tile)
-  __device__ __forceinline__ void load_blk(d4 (&acc)[4][4], const double* M, int ld, int I0, int J0) {
+  __device__ __forceinline__ void load_blk(d4 (&acc)[4][4], gcdbl* M, int ld, int I0, int J0) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int ta = 0; ta < 4; ++ta)
@@ -550,7 +616,7 @@ struct Large {
           acc[ta][tb][r] = M[(int64_t)(J0 + 16 * tb + cl) * ld + I0 + 16 * ta + g + 4 * r];
   }
   // idpad: diagonal entries at index >= idpad are set to 1 (identity padding)
-  __device__ __forceinline__ void store_blk(const d4 (&acc)[4][4], double* M, int ld, int I0, int J0, int idpad) {
+  __device__ __forceinline__ void store_blk(const d4 (&acc)[4][4], gdbl* M, int ld, int I0, int J0, int idpad) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int ta = 0; ta < 4; ++ta)
@@ -580,51 +646,47 @@ struct Large {
   // a wavefront takes CG columns at a time (independent per-cone reductions
   // overlap).  Zero padding (rows >= k, columns >= n).
   __device__ void form_X() {
-    const int KP = L.KP;
+    const int KP = L.KP, ln = lane, kk = k, nn = n;
     for (int j0 = CG * wv; j0 < L.NPAD; j0 += CG * NW) {
-      const double* gc[CG];
-      double* xc[CG];
-      bool live[CG];
-#pragma unroll
-      for (int u = 0; u < CG; ++u) {
-        const int j = j0 + u;
-        live[u] = j < n;
-        gc[u] = Gp + (int64_t)(live[u] ? j : 0) * k;
-        xc[u] = Xw + (int64_t)j * KP;
-      }
-      for (int i = lane; i < kpoc; i += 64) {
+      // column j0 + u of G at g0 + u*k, of X at x0 + u*KP (dead columns read column 0)
+      gcdbl* g0 = Gp + (int64_t)(j0 < nn ? j0 : 0) * kk;
+      gdbl* x0 = Xw + (int64_t)j0 * KP;
+      const int nl = nn - j0;  // live columns: u < nl
+#define GC(u, i) g0[(int64_t)((u) < nl ? (u) : 0) * kk + (i)]
+      for (int i = ln; i < kpoc; i += 64) {
         const double ca = LV(CA + i);
 #pragma unroll
-        for (int u = 0; u < CG; ++u) xc[u][i] = live[u] ? ca * gc[u][i] : 0.0;
+        for (int u = 0; u < CG; ++u) x0[u * KP + i] = (u < nl) ? ca * GC(u, i) : 0.0;
       }
       for (int c = csoc; c < nc; ++c) {
         const int o = a.cones.offs[c], d = a.cones.dim[c];
         double pd[CG];
 #pragma unroll
         for (int u = 0; u < CG; ++u) pd[u] = 0.0;
-        for (int i = o + 1 + lane; i < o + d; i += 64) {
+        for (int i = o + 1 + ln; i < o + d; i += 64) {
           const double wb = LV(WB + i);
 #pragma unroll
-          for (int u = 0; u < CG; ++u) pd[u] = fma(wb, gc[u][i], pd[u]);
+          for (int u = 0; u < CG; ++u) pd[u] = fma(wb, GC(u, i), pd[u]);
         }
         const double im = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
         double cst[CG];
 #pragma unroll
         for (int u = 0; u < CG; ++u) {
           const double del = wave_sum(pd[u]);
-          const double g0 = gc[u][o];
-          cst[u] = -g0 + del * i1;
-          if (lane == 0) xc[u][o] = live[u] ? im * (wb0 * g0 - del) : 0.0;
+          const double gh = GC(u, o);
+          cst[u] = -gh + del * i1;
+          if (ln == 0) x0[u * KP + o] = (u < nl) ? im * (wb0 * gh - del) : 0.0;
         }
-        for (int i = o + 1 + lane; i < o + d; i += 64) {
+        for (int i = o + 1 + ln; i < o + d; i += 64) {
           const double wb = LV(WB + i);
 #pragma unroll
-          for (int u = 0; u < CG; ++u) xc[u][i] = live[u] ? im * (gc[u][i] + cst[u] * wb) : 0.0;
+          for (int u = 0; u < CG; ++u) x0[u * KP + i] = (u < nl) ? im * (GC(u, i) + cst[u] * wb) : 0.0;
         }
       }
-      for (int i = k + lane; i < KP; i += 64) {
+#undef GC
+      for (int i = kk + ln; i < KP; i += 64) {
 #pragma unroll
-        for (int u = 0; u < CG; ++u) xc[u][i] = 0.0;
+        for (int u = 0; u < CG; ++u) x0[u * KP + i] = 0.0;
       }
     }
     BAR();
@@ -655,37 +717,38 @@ struct Large {
   // it in Yp.  Pivot d = the Schur complement = (Cholesky diagonal)^2, so the
   // failure test is the one LAPACK potrf applies (d <= 0 or NaN).  The other
   // blocks get M_IJ -= sum_c rc_c[I]' rc_c[J] / d_c once per panel (MFMA).
-  __device__ bool sweep(double* M, int ld, int nb) {
-    const int rr = wv;
+  template <int nb>
+  __device__ bool sweep_nb(gdbl* M, int ld) {
+    // members copied to locals: the step loop has a barrier in it, after which
+    // members (this is a stack object once sweep is an out-of-line call) would
+    // be reloaded from scratch
+    const int rr = wv, ln = lane, t0 = tid, o_row = L.o_row, RW = L.RW, o_rv = L.o_rv;
+    gdbl* const Y = Yp;
     for (int P = 0; P < nb; ++P) {
       const int P0 = 64 * P;
-      double Z[8][NBT];
+      double Z[8][nb];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int x = P0 + rr + 8 * q;
 #pragma unroll
-        for (int t = 0; t < NBT; ++t) {
-          Z[q][t] = 0.0;
-          if (t < nb) {
-            const int y = 64 * t + lane;
-            Z[q][t] = (y <= x) ? M[(int64_t)y * ld + x] : M[(int64_t)x * ld + y];
-          }
+        for (int t = 0; t < nb; ++t) {
+          const int y = 64 * t + ln;  // element (x, y) from the lower triangle
+          Z[q][t] = M[(y <= x) ? (int64_t)y * ld + x : (int64_t)x * ld + y];
         }
       }
       bool ok = true;
       for (int c = 0; c < 64; ++c) {
-        const int buf = L.o_row + (c & 1) * L.RW;
-        if (wv == (c & 7)) {
+        const int buf = o_row + (c & 1) * RW;
+        if (rr == (c & 7)) {
           const int qc = c >> 3;
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             if (q == qc) {
 #pragma unroll
-              for (int t = 0; t < NBT; ++t)
-                if (t < nb) {
-                  LV(buf + 64 * t + lane) = Z[q][t];
-                  Yp[(int64_t)(64 * t + lane) * 64 + c] = Z[q][t];
-                }
+              for (int t = 0; t < nb; ++t) {
+                LV(buf + 64 * t + ln) = Z[q][t];
+                Y[(int64_t)c * RW + 64 * t + ln] = Z[q][t];  // coalesced row store
+              }
             }
           }
         }
@@ -693,49 +756,59 @@ struct Large {
         const double d = LV(buf + P0 + c);
         ok = ok && (d > 0.0);
         const double r = 1.0 / d;
-        if (tid == 0) LV(L.o_rv + c) = -r;
-        double rowv[NBT], colv[8];
+        if (t0 == 0) LV(o_rv + c) = -r;
+        double rowv[nb], colv[8];
 #pragma unroll
-        for (int t = 0; t < NBT; ++t) rowv[t] = (t < nb) ? LV(buf + 64 * t + lane) : 0.0;
+        for (int t = 0; t < nb; ++t) rowv[t] = LV(buf + 64 * t + ln);
 #pragma unroll
         for (int q = 0; q < 8; ++q) colv[q] = LV(buf + P0 + rr + 8 * q);
-        const int p = P0 + c;
+        // rank-1 update of every element, then the pivot column (block P, lane
+        // c: a select) and the pivot row (one register row of one wavefront)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const bool xr = (rr + 8 * q) == c;
+        for (int q = 0; q < 8; ++q)
 #pragma unroll
-          for (int t = 0; t < NBT; ++t) {
-            if (t < nb) {
-              const bool yc = (64 * t + lane) == p;
-              const double gen = fma(-(colv[q] * rowv[t]), r, Z[q][t]);
-              Z[q][t] = (xr && yc) ? -r : (yc ? colv[q] * r : (xr ? rowv[t] * r : gen));
-            }
+          for (int t = 0; t < nb; ++t) Z[q][t] = fma(-(colv[q] * rowv[t]), r, Z[q][t]);
+        const bool lc = ln == c;
+#pragma unroll
+        for (int t = 0; t < nb; ++t)
+          if (t == P) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) Z[q][t] = lc ? colv[q] * r : Z[q][t];
           }
+        if (rr == (c & 7)) {
+          const int qc = c >> 3;
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (q == qc) {
+#pragma unroll
+              for (int t = 0; t < nb; ++t) Z[q][t] = (t == P && lc) ? -r : rowv[t] * r;
+            }
         }
       }
       BAR();  // Yp and the pivot reciprocals complete
       if (!ok) return false;
+      {
+        // addresses recomputed from a fresh lane id: reusing the load's would
+        // keep 64 of them live (spilled) across the step loop
+        const int lf = lane_fresh() & 63;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int x = P0 + rr + 8 * q;
+        for (int q = 0; q < 8; ++q) {
+          const int x = P0 + rr + 8 * q;
 #pragma unroll
-        for (int t = 0; t < NBT; ++t)
-          if (t < nb) {
-            const int y = 64 * t + lane;
-            if (y <= x)
-              M[(int64_t)y * ld + x] = Z[q][t];
-            else
-              M[(int64_t)x * ld + y] = Z[q][t];
+          for (int t = 0; t < nb; ++t) {
+            const int y = 64 * t + lf;
+            M[(y <= x) ? (int64_t)y * ld + x : (int64_t)x * ld + y] = Z[q][t];
           }
+        }
       }
       const int no = nb - 1, ng = no * (no + 1) / 2;
-      for (int t = wv; t < ng; t += NW) {
+      for (int t = rr; t < ng; t += NW) {
         int a_, b_;
         tri_ij(t, a_, b_);
         const int I = a_ + (a_ >= P ? 1 : 0), J = b_ + (b_ >= P ? 1 : 0);
         d4 acc[4][4];
         load_blk(acc, M, ld, 64 * I, 64 * J);
-        blk_gemm(acc, Yp, Yp, 64, 64 * I, 64 * J, 64, false, L.o_rv);
+        gram_blk(acc, Y, RW, 64 * I, 64 * J, o_rv);
         store_blk(acc, M, ld, 64 * I, 64 * J, NOPAD);
       }
       BAR();
@@ -743,27 +816,43 @@ struct Large {
     return true;
   }
 
+  // nb (= ld / 64) as a template constant: the panel row is then a fixed
+  // register array with no per-element predicates
+  __device__ bool sweep(gdbl* M, int ld) {
+    switch (ld / 64) {
+      case 1: return sweep_nb<1>(M, ld);
+      case 2: return sweep_nb<2>(M, ld);
+      case 3: return sweep_nb<3>(M, ld);
+      case 4: return sweep_nb<4>(M, ld);
+      case 5: return sweep_nb<5>(M, ld);
+      case 6: return sweep_nb<6>(M, ld);
+      case 7: return sweep_nb<7>(M, ld);
+      default: return sweep_nb<8>(M, ld);
+    }
+  }
+
   // M (lower triangle = -X^-1) -> X^-1 in both triangles
-  __device__ void finalize_sym(double* M, int ld) {
-    const int64_t tot = (int64_t)ld * ld;
-    for (int64_t e = tid; e < tot; e += NTH) {
-      const int C = (int)(e / ld), R = (int)(e - (int64_t)C * ld);
-      if (R >= C) {
-        const double v = -M[e];
-        M[e] = v;
+  __device__ void finalize_sym(gdbl* M, int ld) {
+    for (int C = wv; C < ld; C += NW)
+      for (int R = C + lane; R < ld; R += 64) {
+        const double v = -M[(int64_t)C * ld + R];
+        M[(int64_t)C * ld + R] = v;
         if (R != C) M[(int64_t)R * ld + C] = v;
       }
-    }
     BAR();
   }
 
   // setup_iter (densesolver.jl:41-52): H (+A'A), Li = H^-1, T = Li A', S = A T, S^-1
   __device__ int factor(bool addAA, bool h_only) {
+    LSTAMP(SP_OTHER);
     form_X();
+    LSTAMP(SP_U);
     form_H(addAA);
-    if (!sweep(Hm, L.NPAD, L.NPAD / 64)) return ST_CHOL_H;
+    LSTAMP(SP_SYRK);
+    if (!sweep(Hm, L.NPAD)) return ST_CHOL_H;
     if (h_only) return 0;
     finalize_sym(Hm, L.NPAD);
+    LSTAMP(SP_SWEEP_H);
     const int NB = L.NPAD / 64, MB = L.MPAD / 64;
     for (int t = wv; t < NB * MB; t += NW) {
       const int I = t / MB, J = t - I * MB;
@@ -782,8 +871,9 @@ struct Large {
       store_blk(acc, Sm, L.MPAD, 64 * I, 64 * J, m);
     }
     BAR();
-    if (!sweep(Sm, L.MPAD, MB)) return ST_CHOL_S;
+    if (!sweep(Sm, L.MPAD)) return ST_CHOL_S;
     finalize_sym(Sm, L.MPAD);
+    LSTAMP(SP_SCHUR);
     return 0;
   }
 
@@ -791,17 +881,15 @@ struct Large {
   // out[j] = (G' vin)[j] (+ add[j]) for j < n: a wavefront takes CG columns
   __device__ void gemv_Gt(int vin, int vout, int vadd) {
     for (int j0 = CG * wv; j0 < n; j0 += CG * NW) {
-      const double* gc[CG];
+      gcdbl* g0 = Gp + (int64_t)j0 * k;
+      const int nl = n - j0;  // live columns u < nl (dead ones re-read column j0)
       double acc[CG];
 #pragma unroll
-      for (int u = 0; u < CG; ++u) {
-        gc[u] = Gp + (int64_t)(j0 + u < n ? j0 + u : n - 1) * k;
-        acc[u] = 0.0;
-      }
+      for (int u = 0; u < CG; ++u) acc[u] = 0.0;
       for (int i = lane; i < k; i += 64) {
         const double v = LV(vin + i);
 #pragma unroll
-        for (int u = 0; u < CG; ++u) acc[u] = fma(gc[u][i], v, acc[u]);
+        for (int u = 0; u < CG; ++u) acc[u] = fma(g0[(int64_t)(u < nl ? u : 0) * k + i], v, acc[u]);
       }
 #pragma unroll
       for (int u = 0; u < CG; ++u) {
@@ -849,7 +937,7 @@ struct Large {
     return sq;
   }
   // out = M vin for a full symmetric column-major M (thread per row)
-  __device__ void symv(const double* M, int ld, int vin, int vout) {
+  __device__ void symv(gcdbl* M, int ld, int vin, int vout) {
     for (int i = tid; i < ld; i += NTH) {
       double acc = 0.0;
 #pragma unroll 16
@@ -902,7 +990,9 @@ struct Large {
   // solve_socp (solver.jl:40-153) for problem p: the register kernel's control
   // flow and status rules.
   __device__ void run(int64_t p) {
+    LSTAMP(SP_OTHER);
     load(p);
+    LSTAMP(SP_LOAD);
     int status = ST_MAXIT, iters = 0;
     double nd = NAN, np_ = NAN, gap = NAN, ll = 0.0;
     bool dm_aa = false;
@@ -987,9 +1077,13 @@ struct Large {
     }
     int it = 0;
     while (go) {
+      LSTAMP(SP_OTHER);
       residuals(nd, np_, gap);
+      LSTAMP(SP_RESID);
       if (it >= a.maxit) break;
-      if (scaling_op(ll, dm_aa, true)) {
+      const bool dm_it = scaling_op(ll, dm_aa, true);
+      LSTAMP(SP_SCALING);
+      if (dm_it) {
         status = ST_DOMAIN;
         break;
       }
@@ -1009,18 +1103,26 @@ struct Large {
         status = f;
         break;
       }
+      LSTAMP(SP_OTHER);
       solve_head();  // affine direction (solver.jl:125-130)
+      LSTAMP(SP_VOP);
       solve_matrix_part(false);
+      LSTAMP(SP_SOLVE);
       int dom = 0;
       double t = solve_tail(true, dm_aa, dom);
+      LSTAMP(SP_VOP);
       if (dom) {
         status = ST_DOMAIN;
         break;
       }
       affine_post(t, ll);
+      LSTAMP(SP_STEP);
       solve_head();  // combined direction (solver.jl:141-145)
+      LSTAMP(SP_VOP);
       solve_matrix_part(false);
+      LSTAMP(SP_SOLVE);
       t = solve_tail(true, dm_aa, dom);
+      LSTAMP(SP_VOP);
       if (dom) {
         status = ST_DOMAIN;
         break;
@@ -1033,6 +1135,7 @@ struct Large {
         LV(S_ + i) = LV(S_ + i) + LV(RS + i) * stp;
       }
       BAR();
+      LSTAMP(SP_STEP);
       iters = ++it;
     }
     for (int j = tid; j < n; j += NTH) a.x[p * n + j] = LV(X_ + j);
@@ -1051,6 +1154,10 @@ struct Large {
       a.status[p] = status;
     }
     BAR();
+    LSTAMP(SP_STORE);
+#ifdef SOCP_DIAG
+    if (tid == 0) reinterpret_cast<unsigned long long*>(lg_lds + L.o_red + 16)[NSTAMP] += iters;
+#endif
   }
 };
 
@@ -1066,6 +1173,7 @@ __global__ void __launch_bounds__(NTH, 1) socp_large_kernel(LargeArgs args) {
     if (p >= args.a.B) break;
     S.run(p);
   }
+  S.flush_stamps();
 }
 
 }  // namespace lg

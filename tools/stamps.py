@@ -10,7 +10,9 @@ import socp_amd as S
 from socp_amd import _lib
 from socp_amd.configs import CONFIGS
 names = ["load", "scaling", "resid", "U", "SYRK", "sweepH", "schur", "solve", "step", "vop", "store", "other"]
-for cname, B, K in (("C2", 8192, 8), ("C1", 4096, 3)):
+RUNS = {"C2": (8192, 8), "C1": (4096, 3), "C4": (256, 3)}
+for cname in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["C2", "C1"]):
+    B, K = RUNS[cname]
     cfg = CONFIGS[cname]
     ctx = S.default_context()
     c, A, b, G, h = S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
