@@ -547,46 +547,56 @@ struct Small {
   // holds the cone total -- a sum, or a max for the values flagged in MX.  DPP
   // inclusive scan inside each slot, then the segment-end lanes hand their
   // partials over through LDS (a cone may span both slots).
+  // The slots' scans run interleaved step by step (independent DPP chains
+  // hide each other's latency); the DPP moves write every lane, so no old value
+  // is materialised (lanes a pattern leaves unwritten fail the step's
+  // predicate); all partials are read before any is used.
   template <int NV, unsigned MX>
   __device__ __forceinline__ void cone_reduce(double (&v)[2][NV]) {
     LANE_IDS();
+    constexpr int NS = KP > 64 ? 2 : 1;  // slots that can hold elements of this shape
     const int rl = lane & 15;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (64 * s >= k) continue;
-      const int st = ssl[s];
-#define SOCP_SCAN_STEP(CTRL, RM, OK)                             \
-  {                                                              \
-    const bool ok_ = (OK);                                       \
-    _Pragma("unroll") for (int q = 0; q < NV; ++q) {             \
-      const double y = dpp<CTRL, RM>(v[s][q]);                   \
+#define SOCP_SCAN_STEP(CTRL, OK)                                         \
+  _Pragma("unroll") for (int s = 0; s < NS; ++s) {                       \
+    const int st = ssl[s];                                               \
+    const bool ok_ = (OK);                                               \
+    _Pragma("unroll") for (int q = 0; q < NV; ++q) {                     \
+      const double y = dpp_all<CTRL>(v[s][q]);                           \
       const double r = ((MX >> q) & 1) ? fmax(v[s][q], y) : v[s][q] + y; \
-      v[s][q] = ok_ ? r : v[s][q];                               \
-    }                                                            \
+      v[s][q] = ok_ ? r : v[s][q];                                       \
+    }                                                                    \
   }
-      SOCP_SCAN_STEP(0x111, 0xF, rl >= 1 && lane - 1 >= st)
-      SOCP_SCAN_STEP(0x112, 0xF, rl >= 2 && lane - 2 >= st)
-      SOCP_SCAN_STEP(0x114, 0xF, rl >= 4 && lane - 4 >= st)
-      SOCP_SCAN_STEP(0x118, 0xF, rl >= 8 && lane - 8 >= st)
-      SOCP_SCAN_STEP(0x142, 0xA, ((lane >> 4) & 1) && ((lane & ~15) - 1 >= st))
-      SOCP_SCAN_STEP(0x143, 0xC, lane >= 32 && 31 >= st)
+    SOCP_SCAN_STEP(0x111, rl >= 1 && lane - 1 >= st)
+    SOCP_SCAN_STEP(0x112, rl >= 2 && lane - 2 >= st)
+    SOCP_SCAN_STEP(0x114, rl >= 4 && lane - 4 >= st)
+    SOCP_SCAN_STEP(0x118, rl >= 8 && lane - 8 >= st)
+    SOCP_SCAN_STEP(0x142, ((lane >> 4) & 1) && ((lane & ~15) - 1 >= st))
+    SOCP_SCAN_STEP(0x143, lane >= 32 && 31 >= st)
 #undef SOCP_SCAN_STEP
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
       if (lane == sle[s]) {
 #pragma unroll
         for (int q = 0; q < NV; ++q) LDS(O_PART + (q * NCS + ci[s]) * 2 + s) = v[s][q];
       }
     }
     SYNC();
+    double pp[NS][NV][2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (64 * s >= k) continue;
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int q = 0; q < NV; ++q) {
-        const double p0 = LDS(O_PART + (q * NCS + ci[s]) * 2), p1 = LDS(O_PART + (q * NCS + ci[s]) * 2 + 1);
+        pp[s][q][0] = LDS(O_PART + (q * NCS + ci[s]) * 2);
+        pp[s][q][1] = LDS(O_PART + (q * NCS + ci[s]) * 2 + 1);
+      }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        const double p0 = pp[s][q][0], p1 = pp[s][q][1];
         const double both = ((MX >> q) & 1) ? fmax(p0, p1) : p0 + p1;
         v[s][q] = spn[s] ? both : (s == 0 ? p0 : p1);
       }
-    }
   }
 
   __device__ __forceinline__ double ccv(int q, int c) const { return LDS(cc(q, c)); }
@@ -1035,40 +1045,60 @@ struct Small {
     }
   }
 
+  // Pivot data of step C, from the (exactly symmetric) diagonal tile D: column
+  // c by DPP row_newbcast, the pivot by readlane, row c (= column c) by a row
+  // broadcast -- registers only.
+  struct Piv {
+    double cR[4];  // lane (g, cl): D[g + 4r][c]
+    double d, rinv, rowD;
+  };
+  template <int C>
+  __device__ __forceinline__ static void pivot_data(const d4& D, Piv& v) {
+    constexpr int pr = C / 4, pg = C % 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v.cR[r] = dpp_all<0x150 + C>(D[r]);
+    v.d = readlane_d(D[pr], 16 * pg + C);
+    v.rinv = recip(v.d);
+    v.rowD = row_bcast<pg>(D[pr]);
+  }
+
   // Single-pivot steps C.. of panel P (pivot c = 16 P + C, row c of the tile is
-  // register pr of the lanes of row pg).  The lanes of row pg publish row c of
-  // the diagonal tile and of every slab tile through LDS; while those reads are
-  // in flight the pivot column arrives by DPP row_newbcast and the pivot by
-  // readlane.  The diagonal tile is kept exactly symmetric: the rank-1 term is
-  // (D_ic D_cj) / d with one product for (i,j) and (j,i), and the pivot row and
-  // column are the same values times 1/d -- so its row c IS its column c, and
-  // the inverse stays a good right-inverse at kappa ~ 1e10.
+  // register pr of the lanes of row pg).  The pivot data of step C arrive in
+  // pv (computed by the previous step right after its tile update, so the DPP /
+  // readlane / reciprocal chain overlaps the slab work).  The lanes of row pg
+  // publish row c of every slab tile through LDS.  The diagonal tile is kept
+  // exactly symmetric: the rank-1 term is (D_ic D_cj) / d with one product for
+  // (i,j) and (j,i), and the pivot row and column are the same values times
+  // 1/d -- so its row c IS its column c, and the inverse stays a good
+  // right-inverse at kappa ~ 1e10.
   template <int Q, int P, int C>
-  __device__ __forceinline__ void sweep_steps(d4& D, d4 (&Z)[Q], d4 (&W)[Q], d4& rv, int cnt, int& step,
-                                              bool& ok) {
+  __device__ __forceinline__ void sweep_steps(d4& D, d4 (&Z)[Q], d4 (&W)[Q], d4& rv, Piv& pv, int cnt,
+                                              int& step, bool& ok) {
     if constexpr (C < 16) {
       constexpr int pr = C / 4, pg = C % 4;
       if (C >= cnt) return;
       LANE_IDS();
       const bool lane_c = cl == C, lane_r = g == pg;
-      const int cb = O_COL + (step & 1) * SH::CB;
-      ++step;
-      if (lane_r) {
+      double rowv[Q];  // row c of slab tile i at column cl
+      if constexpr (Q > 1) {
+        const int cb = O_COL + (step & 1) * SH::CB;
+        ++step;
+        if (lane_r) {
 #pragma unroll
-        for (int i = 0; i < Q; ++i) LDS(cb + 16 * i + cl) = (i == P) ? D[pr] : Z[i][pr];
+          for (int i = 0; i < Q; ++i)
+            if (i != P) LDS(cb + 16 * i + cl) = Z[i][pr];
+        }
+        SYNC();
+#pragma unroll
+        for (int i = 0; i < Q; ++i)
+          if (i != P) rowv[i] = LDS(cb + 16 * i + cl);
       }
-      SYNC();
-      double rowv[Q];  // row c of tile i at column cl
-#pragma unroll
-      for (int i = 0; i < Q; ++i) rowv[i] = LDS(cb + 16 * i + cl);
-      double cR[4];  // lane (g, cl): D[g + 4r][c]
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cR[r] = dpp_all<0x150 + C>(D[r]);
-      const double d = readlane_d(cR[pr], 16 * pg);
-      ok = ok && (d > 0.0);  // a failed pivot poisons the rest; tested once at the end
-      const double rinv = recip(d);
+      const double cR0 = pv.cR[0], cR1 = pv.cR[1], cR2 = pv.cR[2], cR3 = pv.cR[3];
+      const double cR[4] = {cR0, cR1, cR2, cR3};
+      const double rinv = pv.rinv;
+      ok = ok && (pv.d > 0.0);  // a failed pivot poisons the rest; tested once at the end
       {
-        const double rowD = rowv[P], cC = rowD * rinv;
+        const double rowD = pv.rowD, cC = rowD * rinv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const double gen = fma(-(cR[r] * rowD), rinv, D[r]);
@@ -1077,6 +1107,7 @@ struct Small {
           D[r] = (iR && lane_c) ? -rinv : (lane_c ? scol : (iR ? cC : gen));
         }
       }
+      if constexpr (C + 1 < 16) pivot_data<C + 1>(D, pv);
       rv[pr] = lane_r ? rinv : rv[pr];
 #pragma unroll
       for (int i = 0; i < Q; ++i) {
@@ -1091,7 +1122,7 @@ struct Small {
         }
       }
       SCHED_FENCE();  // no hoisting of the next step's loads/broadcasts across
-      sweep_steps<Q, P, C + 1>(D, Z, W, rv, cnt, step, ok);
+      sweep_steps<Q, P, C + 1>(D, Z, W, rv, pv, cnt, step, ok);
     }
   }
 
@@ -1131,7 +1162,9 @@ struct Small {
       }
       int step = 0;
       bool ok = true;
-      sweep_steps<Q, P, 0>(M[tri(P, P)], Z, W, rv, cnt, step, ok);
+      Piv pv;
+      pivot_data<0>(M[tri(P, P)], pv);
+      sweep_steps<Q, P, 0>(M[tri(P, P)], Z, W, rv, pv, cnt, step, ok);
       if (!ok) return false;
       // M_OO -= sum_c rc_c rc_c' / d_c (lower tiles of every other block row /
       // column); lane (g, cl) of k-step s holds pivot 4s + g
