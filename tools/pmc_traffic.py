@@ -19,7 +19,7 @@ def per_dispatch(d, counter):
     vals = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if "socp_small_kernel" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
+            if not any(kn in r["Kernel_Name"] for kn in ("socp_small_kernel", "socp_large_kernel")) or r["Counter_Name"] != counter:
                 continue
             key = (f, r["Dispatch_Id"])
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
