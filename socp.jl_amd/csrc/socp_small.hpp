@@ -1121,7 +1121,7 @@ struct Small {
           Z[i][r] = (r == pr && lane_r) ? rs : gen;
         }
       }
-      SCHED_FENCE();  // no hoisting of the next step's loads/broadcasts across
+      if constexpr (C % 4 == 3) SCHED_FENCE();  // bound how far the next steps' work is hoisted
       sweep_steps<Q, P, C + 1>(D, Z, W, rv, pv, cnt, step, ok);
     }
   }
