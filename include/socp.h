@@ -157,6 +157,21 @@ int socp_generate(socp_ctx* ctx, const socp_dims* dims,
                   uint64_t seed, int64_t first_problem,
                   double* c, double* A, double* b, double* G, double* h);
 
+/* Ingest: pack a batch of sparse matrices in Julia's
+ * SparseMatrixCSC form -- the storage of Problem.A and Problem.G
+ * (Socp.jl:25,29) -- into the dense column-major batch layout above, on the
+ * device.  Every matrix is rows x cols.  Problem p's nonzeros are
+ * nz_offs[p] .. nz_offs[p+1]-1 of rowval/nzval; its column pointer is
+ * colptr[p*(cols+1) .. p*(cols+1)+cols] (relative to nz_offs[p]).  Indices are
+ * int64 with index_base 1 (Julia, zero-copy) or 0.  All pointers are device
+ * pointers; dense[p*rows*cols + j*rows + i] is written for every element
+ * (zeros included).  Duplicate (i,j) entries are summed, as sparse() does.
+ * Returns SOCP_E_INVALID (after synchronising) if any row index or column
+ * pointer is out of range; nothing else is validated. */
+int socp_pack_csc(socp_ctx* ctx, int64_t batch, int32_t rows, int32_t cols,
+                  const int64_t* nz_offs, const int64_t* colptr, const int64_t* rowval,
+                  const double* nzval, int32_t index_base, double* dense);
+
 /* Timing of the last solve's main kernel, measured with HIP events on the
  * context's stream (milliseconds), and its name. */
 int socp_last_kernel_ms(socp_ctx* ctx, float* ms);

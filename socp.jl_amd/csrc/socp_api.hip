@@ -57,7 +57,7 @@ struct socp_ctx {
   float last_ms = 0.f;
   const char* last_name = "";
   enum { B_C, B_A, B_B, B_G, B_H, B_SING, B_X, B_Y, B_Z, B_S, B_IT, B_ST, B_RES, B_DX, B_DY,
-         B_DZ, B_DS, B_CX, B_CY, B_CZ, B_CS, B_CNT, B_LWS, NB };
+         B_DZ, B_DS, B_CX, B_CY, B_CZ, B_CS, B_CNT, B_LWS, B_ERR, NB };
   DevBuf buf[NB];
 };
 
@@ -595,5 +595,73 @@ extern "C" int socp_generate(socp_ctx* ctx, const socp_dims* dims, const int32_t
   void* kargs[] = {&a};
   HIPCHK(hipLaunchKernel((const void*)&socp_generate_kernel, dim3((unsigned)a.B), dim3(256), kargs,
                          sh, ctx->stream));
+  return 0;
+}
+
+// --------------------------------------------------------------- ingest
+// socp_pack_csc: one workgroup per problem; the problem's dense block is
+// zeroed by the workgroup, then every thread scatters a strided share of the
+// nonzeros (column by column: the column of nonzero e is found by a binary
+// search of colptr, so the scatter is one pass over nz).  Duplicates are
+// summed with atomics only where they occur: a nonzero whose predecessor in
+// the same column has the same row index adds instead of storing.
+namespace {
+__global__ void __launch_bounds__(256) socp_pack_csc_kernel(int32_t rows, int32_t cols, const int64_t* nz_offs,
+                                                           const int64_t* colptr, const int64_t* rowval,
+                                                           const double* nzval, int64_t base, double* dense,
+                                                           int32_t* err) {
+  const int64_t p = blockIdx.x;
+  const int64_t rc = (int64_t)rows * cols;
+  double* D = dense + p * rc;
+  for (int64_t e = threadIdx.x; e < rc; e += blockDim.x) D[e] = 0.0;
+  __syncthreads();
+  const int64_t* cp = colptr + p * (int64_t)(cols + 1);
+  const int64_t n0 = nz_offs[p], nnz = nz_offs[p + 1] - n0;
+  if (cp[0] - base != 0 || cp[cols] - base != nnz) {
+    if (threadIdx.x == 0) atomicOr(err, 1);
+    return;
+  }
+  for (int64_t e = threadIdx.x; e < nnz; e += blockDim.x) {
+    // column j: the last j with cp[j] - base <= e
+    int lo = 0, hi = cols;  // invariant: cp[lo] - base <= e < cp[hi] - base
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (cp[mid] - base <= e) lo = mid; else hi = mid;
+    }
+    const int64_t i = rowval[n0 + e] - base;
+    if (i < 0 || i >= rows) {
+      atomicOr(err, 2);
+      continue;
+    }
+    const bool dup = e > cp[lo] - base && rowval[n0 + e - 1] - base == i;
+    const bool has_dup_after = e + 1 < cp[lo + 1] - base && rowval[n0 + e + 1] - base == i;
+    if (dup || has_dup_after)
+      atomicAdd(D + (int64_t)lo * rows + i, nzval[n0 + e]);
+    else
+      D[(int64_t)lo * rows + i] = nzval[n0 + e];
+  }
+}
+}  // namespace
+
+extern "C" int socp_pack_csc(socp_ctx* ctx, int64_t batch, int32_t rows, int32_t cols, const int64_t* nz_offs,
+                             const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                             int32_t index_base, double* dense) {
+  if (!ctx) return fail(SOCP_E_INVALID, "ctx is NULL");
+  if (batch < 0 || rows < 0 || cols < 0 || (index_base != 0 && index_base != 1))
+    return fail(SOCP_E_INVALID, "bad batch/rows/cols/index_base");
+  if (batch == 0 || (int64_t)rows * cols == 0) return 0;
+  if (!nz_offs || !colptr || !dense) return fail(SOCP_E_INVALID, "NULL pointer");
+  HIPCHK(hipSetDevice(ctx->device));
+  if (ctx->buf[socp_ctx::B_ERR].ensure(256)) return fail(SOCP_E_NOMEM, "device allocation failed");
+  int32_t* err = (int32_t*)ctx->buf[socp_ctx::B_ERR].p;
+  HIPCHK(hipMemsetAsync(err, 0, sizeof(int32_t), ctx->stream));
+  hipLaunchKernelGGL(socp_pack_csc_kernel, dim3((unsigned)batch), dim3(256), 0, ctx->stream, rows, cols, nz_offs,
+                     colptr, rowval, nzval, (int64_t)index_base, dense, err);
+  HIPCHK(hipGetLastError());
+  int32_t herr = 0;
+  HIPCHK(hipMemcpyAsync(&herr, err, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (herr & 1) return fail(SOCP_E_INVALID, "colptr does not span the problem's nonzeros");
+  if (herr & 2) return fail(SOCP_E_INVALID, "row index out of range");
   return 0;
 }

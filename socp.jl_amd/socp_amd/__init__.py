@@ -25,7 +25,7 @@ from ._lib import (CHOL_H_FAILED, CHOL_S_FAILED, CONE_POC, CONE_SOC, CONVERGED, 
 __all__ = [
     "POC", "SOC", "Problem", "State", "Scaling", "DenseSolver", "HipDenseSolver", "SolverState",
     "solve_socp", "solve_socp_batched", "compute_scaling", "setup_iter", "solve_kkt",
-    "PosDefException", "DomainError", "batch_solve", "batch_kkt_solve", "generate",
+    "PosDefException", "DomainError", "batch_solve", "batch_kkt_solve", "generate", "pack_csc",
     "Context", "SocpError", "default_context", "cone_arrays",
     "CONVERGED", "MAXIT", "CHOL_H_FAILED", "CHOL_S_FAILED", "DOMAIN_ERROR",
 ]
@@ -197,6 +197,42 @@ def generate(cones, B, n, m, k, seed, first_problem=0, *, ctx=None, device=None)
     _lib.check(_lib.load().socp_generate(ctx.handle, dims, p(kind), p(offs), p(dim), seed,
                                          first_problem, p(c), p(A), p(b), p(G), p(h)))
     return c, A[:B * m * n], b[:B * m], G, h
+
+
+def pack_csc(mats, rows=None, cols=None, *, index_base=1, ctx=None, device=None):
+    """Ingest: pack sparse matrices in SparseMatrixCSC form --
+    the storage of Problem.A / Problem.G (Socp.jl:25,29) -- into the dense
+    column-major batch layout on the device (socp_pack_csc).  `mats` is a list
+    of scipy.sparse matrices (CSC after conversion), or a tuple of device int64
+    tensors (nz_offs, colptr, rowval) plus a float64 nzval tensor with rows, cols
+    given.  Returns a flat torch float64 tensor of B*rows*cols."""
+    import torch
+    ctx = ctx or default_context()
+    dev = device or torch.device("cuda", ctx.device)
+    if isinstance(mats, tuple):
+        nz_offs, colptr, rowval, nzval = mats
+        B = nz_offs.numel() - 1
+    else:
+        csc = [m.tocsc() for m in mats]
+        B = len(csc)
+        rows, cols = csc[0].shape if B else (rows or 0, cols or 0)
+        for m in csc:
+            assert m.shape == (rows, cols)
+        nnz = np.array([0] + [m.nnz for m in csc], dtype=np.int64)
+        nz = np.cumsum(nnz)
+        i64 = dict(dtype=torch.int64, device=dev)
+        nz_offs = torch.tensor(nz, **i64)
+        colptr = torch.tensor(np.concatenate([m.indptr.astype(np.int64) + index_base for m in csc])
+                              if B else np.zeros(0, np.int64), **i64)
+        rowval = torch.tensor(np.concatenate([m.indices.astype(np.int64) + index_base for m in csc])
+                              if B and nz[-1] else np.zeros(1, np.int64), **i64)
+        nzval = torch.tensor(np.concatenate([m.data.astype(np.float64) for m in csc])
+                             if B and nz[-1] else np.zeros(1), dtype=torch.float64, device=dev)
+    out = torch.empty(max(B * rows * cols, 1), dtype=torch.float64, device=dev)
+    p = _lib.ptr
+    _lib.check(_lib.load().socp_pack_csc(ctx.handle, B, rows, cols, p(nz_offs), p(colptr), p(rowval),
+                                         p(nzval), index_base, p(out)))
+    return out[:B * rows * cols]
 
 
 # ------------------------------------------------- reference-shaped mirror

@@ -25,7 +25,7 @@ EXPORTED = [
     "socp_ctx_destroy", "socp_ctx_sync", "socp_ctx_stream", "socp_supported",
     "socp_batch_solve", "socp_batch_solve_ex", "socp_batch_kkt_solve", "socp_generate",
     "socp_last_kernel_ms", "socp_last_kernel_name", "socp_debug_set_kkt_dump",
-    "socp_debug_set_stamps",
+    "socp_debug_set_stamps", "socp_pack_csc",
 ]
 
 
@@ -93,6 +93,7 @@ def load():
     L.socp_last_kernel_name.restype = C.c_char_p
     L.socp_debug_set_kkt_dump.argtypes = [vp]
     L.socp_debug_set_stamps.argtypes = [vp]
+    L.socp_pack_csc.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_int32, vp]
     _lib = L
     return L
 

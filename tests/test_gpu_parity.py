@@ -311,3 +311,35 @@ def test_full_size_c2_properties(oracle):
         pc, pA, pb, pG, ph = batch_problem(flat, B, cfg.n, cfg.m, cfg.k, p)
         r = oracle.solve_trace(cfg.cones, pc, pA, pb, pG, ph, sing=False, params=oracle.Params(maxit=8, tol=0.0))
         assert rel(out["x"][p * cfg.n:(p + 1) * cfg.n].cpu().numpy(), r["x"]) <= 1e-6
+
+
+# ------------------------------------------------------------- ingest (§8(f))
+def test_pack_csc_matches_dense():
+    """SparseMatrixCSC -> dense column-major batch (socp_pack_csc), bit-exact
+    against scipy's toarray(); Julia's 1-based indices and 0-based ones; empty
+    columns, an all-zero matrix, a duplicate entry (summed), and a bad index."""
+    import scipy.sparse as sp
+    import torch
+    rng = np.random.default_rng(5)
+    rows, cols = 96, 64
+    mats = [sp.random(rows, cols, density=d, random_state=int(rng.integers(1 << 30)), format="csc")
+            for d in (0.05, 0.3, 0.0, 1.0)]
+    mats[0][:, 7] = 0.0  # an empty column
+    mats[0].eliminate_zeros()
+    want = np.concatenate([m.toarray().ravel(order="F") for m in mats])
+    for base in (1, 0):
+        got = S.pack_csc(mats, index_base=base).cpu().numpy()
+        assert np.array_equal(got, want), base
+    # duplicates are summed (sparse() semantics)
+    dup = sp.csc_matrix((np.array([1.0, 2.0, 4.0]), np.array([3, 3, 5]), np.array([0, 3] + [3] * (cols - 1))),
+                        shape=(rows, cols))
+    got = S.pack_csc([dup]).cpu().numpy().reshape(cols, rows).T
+    assert got[3, 0] == 3.0 and got[5, 0] == 4.0 and np.count_nonzero(got) == 2
+    # a row index out of range is an API error
+    dev = torch.device("cuda", 0)
+    i64 = dict(dtype=torch.int64, device=dev)
+    bad = (torch.tensor([0, 1], **i64), torch.tensor([1] + [2] * cols, **i64), torch.tensor([rows + 1], **i64),
+           torch.ones(1, dtype=torch.float64, device=dev))
+    with pytest.raises(S.SocpError) as e:
+        S.pack_csc(bad, rows, cols)
+    assert e.value.code == -1
