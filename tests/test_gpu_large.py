@@ -163,3 +163,74 @@ def test_c4_full_batch_properties():
             assert (arr[okp, o] > np.linalg.norm(arr[okp, o + 1:o + 80], axis=1)).all(), (key, o)
     res = out["res"].cpu().numpy().reshape(B, 3)
     assert np.isfinite(res[okp]).all()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_large_random_shapes(oracle, seed):
+    """Shapes only the blocked kernel runs (n or m > 64 or k > 128), random cone
+    lists (POC block then SOC cones): first two iterations vs the oracle."""
+    from problems import random_cones
+    rng = np.random.default_rng(700 + seed)
+    n = int(rng.integers(65, 161))
+    m = int(rng.integers(0, min(90, n - 8)))  # m < n: A with more rows than columns is ill-posed
+    k = int(rng.integers(n + 1, 260))
+    cones = random_cones(rng, k)
+    B = 3
+    d = oracle.generate(cones, B, n, m, k, 4242 + seed)
+    r = oracle.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                           params=oracle.Params(maxit=2, tol=0.0))
+    g = S.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"], None, maxit=2, tol=0.0)
+    assert S.default_context().last_kernel_name() == "socp_large_kernel"
+    assert (g["status"] == r["status"]).all(), (n, m, k, len(cones))
+    for p in range(B):
+        if r["status"][p] != S.MAXIT:
+            continue
+        e = rel(g["x"][p * n:(p + 1) * n], r["x"][p * n:(p + 1) * n])
+        assert e <= 1e-8, (n, m, k, len(cones), p, e)
+
+
+def test_large_batch_vs_single_and_warm_start(oracle):
+    """Per-problem determinism of the blocked kernel (bitwise batch == single) and
+    warm start (2 + 3 iterations == 5), at an n=96 shape."""
+    cones, n, m, k = [(0, 0, 40), (1, 40, 60), (1, 100, 60)], 96, 20, 160
+    B = 6
+    d = oracle.generate(cones, B, n, m, k, 99)
+    full = S.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"], None, maxit=5, tol=0.0)
+    p = 4
+    sl = lambda a, L: a[p * L:(p + 1) * L]  # noqa: E731
+    one = S.batch_solve(cones, n, m, k, sl(d["c"], n), sl(d["A"], m * n), sl(d["b"], m), sl(d["G"], k * n),
+                        sl(d["h"], k), None, maxit=5, tol=0.0)
+    assert np.array_equal(one["x"], sl(full["x"], n)) and np.array_equal(one["s"], sl(full["s"], k))
+    a2 = S.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"], None, maxit=2, tol=0.0)
+    a5 = S.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"], None, maxit=3, tol=0.0,
+                       warm=(a2["x"], a2["y"], a2["z"], a2["s"]))
+    assert np.array_equal(a5["x"], full["x"]) and np.array_equal(a5["z"], full["z"])
+
+
+def test_large_kkt_backward_error(oracle):
+    """P6 for the blocked kernel: block-row residuals of the KKT system at a
+    healthy iterate of an n=128 problem, within 10x the oracle's own."""
+    from problems import batch_problem
+    cones, n, m, k = [(1, 0, 100), (1, 100, 100)], 128, 32, 200
+    d = oracle.generate(cones, 1, n, m, k, 77)
+    c, A, b, G, h = batch_problem(d, 1, n, m, k, 0)
+    tr = oracle.solve_trace(cones, c, A, b, G, h, params=oracle.Params(maxit=3, tol=0.0), max_trace=4)
+    x, y, z, s = tr["trace"][2]
+    rng = np.random.default_rng(3)
+    rhs = [rng.standard_normal(q) for q in (n, m, k, k)]
+    out = S.batch_kkt_solve(cones, n, m, k, A.ravel(order="F"), G.ravel(order="F"), np.zeros(1, np.uint8), s, z, *rhs)
+    sc = oracle.compute_scaling(cones, s, z)
+    W, lam = sc["W"], sc["l"]
+
+    def backward(cx, cy, cz, cs):
+        r1 = A.T @ cy + G.T @ cz - rhs[0]
+        r2 = A @ cx - rhs[1]
+        r3 = G @ cx + cs - rhs[2]
+        r4 = oracle.vprod(cones, lam, W @ cz + np.linalg.solve(W.T, cs)) - rhs[3]
+        scale = max(np.abs(np.concatenate(rhs)).max(), np.abs(np.concatenate([cx, cy, cz, cs])).max())
+        return max(np.abs(q).max() for q in (r1, r2, r3, r4)) / scale
+
+    o = oracle.kkt_single(cones, A, G, False, s, z, *rhs)
+    ref_err = backward(o["cx"], o["cy"], o["cz"], o["cs"])
+    assert out["status"][0] == 0
+    assert backward(out["cx"], out["cy"], out["cz"], out["cs"]) <= max(1e-12, 10 * ref_err), ref_err
