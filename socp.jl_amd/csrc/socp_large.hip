@@ -529,6 +529,8 @@ struct Large {
   // step s, lane group g feeds k-row k0 + 4g + s (the k order is free), so a
   // lane's operands are 4 consecutive doubles (two 16-byte loads).  qs >= 0:
   // the Q operand of k-row kk is scaled by LDS[qs + kk].
+  // LO: a diagonal block, whose tiles above the diagonal are not needed (skipped)
+  template <bool LO = false>
   __device__ __forceinline__ void blk_gemm(d4 (&acc)[4][4], gcdbl* P, gcdbl* Q, int ld, int I0,
                                            int J0, int kr, bool same, int qs) {
     const int g = lane >> 4, cl = lane & 15;
@@ -572,13 +574,15 @@ struct Large {
 #pragma unroll
         for (int ta = 0; ta < 4; ++ta)
 #pragma unroll
-          for (int tb = 0; tb < 4; ++tb) acc[ta][tb] = mfma(av[ta][s], bv[tb][s], acc[ta][tb]);
+          for (int tb = 0; tb < 4; ++tb)
+            if (!LO || tb <= ta) acc[ta][tb] = mfma(av[ta][s], bv[tb][s], acc[ta][tb]);
     }
   }
 
   // acc[ta][tb] += sum_{c<64} Y[c][I0+16ta+i] * (LDS[qs+c] * Y[c][J0+16tb+j]) for the
   // row-major 64-row panel Y (row c at Y + c*ld): the sweep's deferred Gram update.
   // At MFMA step s, lane group g feeds row k0 + 4s + g (C/D row order).
+  template <bool LO = false>
   __device__ __forceinline__ void gram_blk(d4 (&acc)[4][4], gcdbl* Y, int ld, int I0, int J0, int qs) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll 1
@@ -599,12 +603,14 @@ struct Large {
 #pragma unroll
         for (int ta = 0; ta < 4; ++ta)
 #pragma unroll
-          for (int tb = 0; tb < 4; ++tb) acc[ta][tb] = mfma(av[ta][s], bv[tb][s], acc[ta][tb]);
+          for (int tb = 0; tb < 4; ++tb)
+            if (!LO || tb <= ta) acc[ta][tb] = mfma(av[ta][s], bv[tb][s], acc[ta][tb]);
     }
   }
 
   // 64x64 block (I0, J0) of a column-major matrix <-> the f64 MFMA C/D layout
   // (lane (g, cl) holds rows g + 4r, column cl of each 16x16 tile)
+  template <bool LO = false>
   __device__ __forceinline__ void load_blk(d4 (&acc)[4][4], gcdbl* M, int ld, int I0, int J0) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
@@ -613,9 +619,10 @@ struct Large {
       for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          acc[ta][tb][r] = M[(int64_t)(J0 + 16 * tb + cl) * ld + I0 + 16 * ta + g + 4 * r];
+          acc[ta][tb][r] = (LO && tb > ta) ? 0.0 : M[(int64_t)(J0 + 16 * tb + cl) * ld + I0 + 16 * ta + g + 4 * r];
   }
   // idpad: diagonal entries at index >= idpad are set to 1 (identity padding)
+  template <bool LO = false>
   __device__ __forceinline__ void store_blk(const d4 (&acc)[4][4], gdbl* M, int ld, int I0, int J0, int idpad) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
@@ -624,6 +631,7 @@ struct Large {
       for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          if (LO && tb > ta) continue;
           const int R = I0 + 16 * ta + g + 4 * r, Cc = J0 + 16 * tb + cl;
           const double v = (R == Cc && R >= idpad) ? 1.0 : acc[ta][tb][r];
           M[(int64_t)Cc * ld + R] = v;
@@ -701,9 +709,15 @@ struct Large {
       tri_ij(t, I, J);
       d4 acc[4][4];
       zero_blk(acc);
-      blk_gemm(acc, Xw, Xw, L.KP, 64 * I, 64 * J, L.KP, I == J, -1);
-      if (addAA) blk_gemm(acc, Ap, Ap, L.MPAD, 64 * I, 64 * J, L.MPAD, I == J, -1);
-      store_blk(acc, Hm, L.NPAD, 64 * I, 64 * J, n);
+      if (I == J) {  // diagonal block: only the tiles on and below the diagonal
+        blk_gemm<true>(acc, Xw, Xw, L.KP, 64 * I, 64 * J, L.KP, true, -1);
+        if (addAA) blk_gemm<true>(acc, Ap, Ap, L.MPAD, 64 * I, 64 * J, L.MPAD, true, -1);
+        store_blk<true>(acc, Hm, L.NPAD, 64 * I, 64 * J, n);
+      } else {
+        blk_gemm(acc, Xw, Xw, L.KP, 64 * I, 64 * J, L.KP, false, -1);
+        if (addAA) blk_gemm(acc, Ap, Ap, L.MPAD, 64 * I, 64 * J, L.MPAD, false, -1);
+        store_blk(acc, Hm, L.NPAD, 64 * I, 64 * J, n);
+      }
     }
     BAR();
   }
@@ -807,9 +821,15 @@ struct Large {
         tri_ij(t, a_, b_);
         const int I = a_ + (a_ >= P ? 1 : 0), J = b_ + (b_ >= P ? 1 : 0);
         d4 acc[4][4];
-        load_blk(acc, M, ld, 64 * I, 64 * J);
-        gram_blk(acc, Y, RW, 64 * I, 64 * J, o_rv);
-        store_blk(acc, M, ld, 64 * I, 64 * J, NOPAD);
+        if (I == J) {
+          load_blk<true>(acc, M, ld, 64 * I, 64 * J);
+          gram_blk<true>(acc, Y, RW, 64 * I, 64 * J, o_rv);
+          store_blk<true>(acc, M, ld, 64 * I, 64 * J, NOPAD);
+        } else {
+          load_blk(acc, M, ld, 64 * I, 64 * J);
+          gram_blk(acc, Y, RW, 64 * I, 64 * J, o_rv);
+          store_blk(acc, M, ld, 64 * I, 64 * J, NOPAD);
+        }
       }
       BAR();
     }
