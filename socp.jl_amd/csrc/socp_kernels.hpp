@@ -24,7 +24,7 @@ constexpr int LARGE_NB_MAX = 8;  // NPAD, MPAD <= 512: a swept panel row lives i
 struct LargeLayout {
   int NPAD, MPAD, KP, RW;  // n, m rounded up to 64, k to 16; RW = max(NPAD, MPAD)
   // LDS offsets (doubles)
-  int o_rc, o_cc, o_kv, o_nv, o_mv, o_row, o_rv, o_part, o_red, total;
+  int o_rc, o_cc, o_kv, o_nv, o_mv, o_row, o_rv, o_part, o_red, o_fx, total;
   // workspace-slot offsets (doubles)
   int64_t w_x, w_h, w_ap, w_at, w_yp, w_t, w_s, w_total;
 };
@@ -45,6 +45,7 @@ __host__ __device__ inline LargeLayout large_layout(int n, int m, int k) {
   L.o_rv = o;   o += 64;            // sweep: -1/d of the panel's pivots
   L.o_part = o; o += 8 * L.MPAD;    // A x partial sums per wavefront
   L.o_red = o;  o += 64;            // block reductions
+  L.o_fx = o;   o += 8 * 64;        // W^-1 G fast path: per wavefront, per-cone sums and heads
   L.total = o;
   int64_t w = 0;
   L.w_x = w;  w += large_al((int64_t)L.KP * L.NPAD);    // X = W^-1 G

@@ -653,6 +653,87 @@ struct Large {
   // X[:, j] = W^-1 G[:, j] (iscale!, scalings.jl:145-173) for every column:
   // a wavefront takes CG columns at a time (independent per-cone reductions
   // overlap).  Zero padding (rows >= k, columns >= n).
+  // W^-1 G fast path (at most FX_NC SOC cones, k <= 64 * FX_R; any POC block):
+  // a wavefront takes FX_CG columns at a time and loads them whole (one HBM
+  // round trip per pass), reduces every cone's wbar-weighted tail sum from
+  // registers, and writes the columns of X.  Otherwise form_X.
+  static constexpr int FX_CG = 4, FX_NC = 8, FX_R = 10;
+  __device__ bool form_X_fast() {
+    const int nsoc = nc - csoc;
+    const int R = (k + 63) / 64;
+    if (nsoc > FX_NC || R > FX_R) return false;
+    const int KP = L.KP, ln = lane, kk = k, nn = n;
+    const int fx = L.o_fx + wv * 64;  // [0,32): del[u][c], [32,64): head value g0[u][c]
+    for (int j0 = FX_CG * wv; j0 < L.NPAD; j0 += FX_CG * NW) {
+      const int nl = nn - j0;
+      gcdbl* g0p = Gp + (int64_t)(j0 < nn ? j0 : 0) * kk;
+      gdbl* x0 = Xw + (int64_t)j0 * KP;
+      double gv[FX_CG][FX_R], wbr[FX_R];
+#pragma unroll
+      for (int r = 0; r < FX_R; ++r) {
+        const int row = ln + 64 * r;
+        const bool in = r < R && row < kk;
+        wbr[r] = in ? LV(WB + row) : 0.0;
+#pragma unroll
+        for (int u = 0; u < FX_CG; ++u) gv[u][r] = in ? g0p[(int64_t)(u < nl ? u : 0) * kk + row] : 0.0;
+      }
+      // per SOC cone: del = sum over the tail of wbar_i G_ij
+#pragma unroll
+      for (int ci = 0; ci < FX_NC; ++ci) {
+        if (ci >= nsoc) break;
+        const int c = csoc + ci, o = a.cones.offs[c], d = a.cones.dim[c];
+        double pd[FX_CG];
+#pragma unroll
+        for (int u = 0; u < FX_CG; ++u) pd[u] = 0.0;
+#pragma unroll
+        for (int r = 0; r < FX_R; ++r) {
+          const int row = ln + 64 * r;
+          const double w = (row > o && row < o + d) ? wbr[r] : 0.0;
+#pragma unroll
+          for (int u = 0; u < FX_CG; ++u) pd[u] = fma(w, gv[u][r], pd[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < FX_CG; ++u) {
+          const double del = wave_sum(pd[u]);
+          if (ln == 0) {
+            LV(fx + u * FX_NC + ci) = del;
+            LV(fx + 32 + u * FX_NC + ci) = g0p[(int64_t)(u < nl ? u : 0) * kk + o];
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int r = 0; r < FX_R; ++r) {
+        const int row = ln + 64 * r;
+        if (r * 64 >= KP) break;
+        const int code = row < kk ? (int)LV(L.o_rc + row) : 3;
+        const int c = code >> 2, typ = code & 3, ci = c - csoc;
+        const bool soc = typ == 1 || typ == 2;
+        const double ca = typ == 0 ? LV(CA + row) : 0.0;
+        const double im = soc ? ccv(CC_IMU, c) : 0.0, wb0 = soc ? ccv(CC_WB0, c) : 0.0,
+                     i1 = soc ? ccv(CC_I1, c) : 0.0;
+#pragma unroll
+        for (int u = 0; u < FX_CG; ++u) {
+          const double del = soc ? LV(fx + u * FX_NC + ci) : 0.0, gh = soc ? LV(fx + 32 + u * FX_NC + ci) : 0.0;
+          const double g = gv[u][r];
+          double x = 0.0;
+          if (typ == 0) x = ca * g;
+          if (typ == 1) x = im * (wb0 * g - del);
+          if (typ == 2) x = im * (g + (-gh + del * i1) * wbr[r]);
+          if (u >= nl) x = 0.0;
+          if (row < KP) x0[u * KP + row] = x;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    BAR();
+    return true;
+  }
+
   __device__ void form_X() {
     const int KP = L.KP, ln = lane, kk = k, nn = n;
     for (int j0 = CG * wv; j0 < L.NPAD; j0 += CG * NW) {
@@ -865,7 +946,7 @@ struct Large {
   // setup_iter (densesolver.jl:41-52): H (+A'A), Li = H^-1, T = Li A', S = A T, S^-1
   __device__ int factor(bool addAA, bool h_only) {
     LSTAMP(SP_OTHER);
-    form_X();
+    if (!form_X_fast()) form_X();
     LSTAMP(SP_U);
     form_H(addAA);
     LSTAMP(SP_SYRK);
