@@ -3,7 +3,7 @@ diagnostic build libsocp_diag.so (SOCP_STAMPS).  Diagnostic only: its run time
 is not a benchmark number (stamps serialise the waits)."""
 import os, sys, time
 HERE = os.path.dirname(os.path.abspath(__file__))
-os.environ["SOCP_AMD_LIB"] = os.path.join(HERE, "..", "socp.jl_amd", "lib", "libsocp_diag.so")
+os.environ.setdefault("SOCP_AMD_LIB", os.path.join(HERE, "..", "socp.jl_amd", "lib", "libsocp_diag.so"))
 sys.path.insert(0, os.path.join(HERE, "..", "socp.jl_amd"))
 import torch
 import socp_amd as S
