@@ -30,6 +30,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "socp.jl_amd"))
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 (vector = matrix), spec
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, spec
 
 
 def flops_per_problem_iter(n, m, k, sing=False):
@@ -56,7 +57,7 @@ def cone_str(cones):
     return "+".join(out)
 
 
-def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None):
+def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None, tol=0.0):
     """Oracle (the reference algorithm restated in C, oracle/) on host cores."""
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle as O  # test infrastructure: timed as the baseline, never the product
@@ -64,7 +65,7 @@ def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None):
     # one batch of a few seconds: 256 problems at C1/C2, one per thread at C4
     chunk = 256 if flops_per_problem_iter(cfg.n, cfg.m, cfg.k) < 1e7 else threads
     d = O.generate(cfg.cones, chunk, cfg.n, cfg.m, cfg.k, cfg.seed)
-    P = O.Params(maxit=fixed_k, tol=0.0)
+    P = O.Params(maxit=fixed_k, tol=tol)
     sing = [0] * chunk
     O.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"], sing=sing,
                   params=P, nthreads=threads)  # warm-up
@@ -78,8 +79,9 @@ def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None):
             break
     dt = time.perf_counter() - t0
     return {"value": iters / dt, "unit": "problem-iterations/s", "cores": threads, "kind": "port",
-            "sample": f"{reps}x{chunk} {cfg.name} problems (first {chunk} of the seeded workload), fixed-K={fixed_k}, "
-                      f"oracle/socp_oracle.c (reference op order incl. dense iW*iW' and potrs(I) inverse), "
+            "sample": f"{reps}x{chunk} {cfg.name} problems (first {chunk} of the seeded workload), "
+                      + (f"tol={tol}, maxit={fixed_k}, " if tol else f"fixed-K={fixed_k}, ")
+                      + f"oracle/socp_oracle.c (reference op order incl. dense iW*iW' and potrs(I) inverse), "
                       f"OpenMP {threads} threads, {dt:.1f}s"}
 
 
@@ -91,6 +93,9 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--batch", type=int, default=0, help="problems per GPU (default: config batch)")
     ap.add_argument("--fixed-k", type=int, default=0)
+    ap.add_argument("--mode", choices=["fixed", "reference"], default="fixed",
+                    help="fixed: tol=0, K iterations (headline, SURVEY.md §8(d)(i)); reference: the "
+                         "reference's stopping rule, tol=1e-5 absolute, maxit=40, per-problem masking (§8(d)(ii))")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "r01_pmc_traffic.json"))
@@ -112,7 +117,9 @@ def main():
 
     cfg = CONFIGS["C2" if args.config == "C3" else args.config]
     B = args.batch or cfg.batch
-    K = args.fixed_k or cfg.fixed_k
+    ref_rule = args.mode == "reference"
+    K = 40 if ref_rule else (args.fixed_k or cfg.fixed_k)  # solver.jl:105
+    tol = 1e-5 if ref_rule else 0.0  # solver.jl:122
     n, m, k = cfg.n, cfg.m, cfg.k
     ctx = S.Context(local)
     c, A, b, G, h = S.generate(cfg.cones, B, n, m, k, cfg.seed, first_problem=rank * B, ctx=ctx)
@@ -123,7 +130,7 @@ def main():
 
     def step():
         nonlocal out
-        out = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=0.0, ctx=ctx, out=out)
+        out = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=tol, ctx=ctx, out=out)
         if world > 1:
             ctx.sync()
             local_st = torch.stack([out["status"], out["iters"]], dim=1)
@@ -161,7 +168,14 @@ def main():
         kms = sum(kernel_ms) / len(kernel_ms)
         iters_per_launch = int(out["iters"].sum().item())
         F = flops_per_problem_iter(n, m, k)
-        achieved = F * iters_per_launch / (kms * 1e-3) / 1e12
+        Bq = bytes_per_problem_iter(n, m, k)
+        # binding bound of the algorithmic model: FP64 when F/B is above the
+        # ridge (C2, C4), HBM below it (C1)
+        hbm_bound = F / Bq < FP64_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+        if hbm_bound:
+            achieved, peak, unit = Bq * iters_per_launch / (kms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
+        else:
+            achieved, peak, unit = F * iters_per_launch / (kms * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
         traffic = None
         if os.path.exists(args.traffic_json):
             try:
@@ -185,7 +199,9 @@ def main():
             "data": "synthetic (device SplitMix64 generator, SURVEY.md §8(d); feasible by construction)",
             "config": {
                 "workload": f"{cfg.name}: {B} problems per GPU, n={n}, m={m}, k={k}, cones {cone_str(cfg.cones)}, "
-                            f"initial point + fixed-K={K} IPM iterations (tol=0)",
+                            + (f"initial point + reference stopping rule (tol=1e-5 abs, maxit={K}; "
+                               f"value counts executed iterations)" if ref_rule else
+                               f"initial point + fixed-K={K} IPM iterations (tol=0)"),
                 "global_batch": B * world,
                 "parallelism": f"dp{world} (disjoint problem shards, status all-gather only)",
             },
@@ -193,18 +209,19 @@ def main():
             "kernel_ms": kms,
             "status_counts": status_counts,
             "roofline": {
-                "bound": "mfma",
+                "bound": "hbm" if hbm_bound else "mfma",
                 "achieved": achieved,
-                "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved / FP64_PEAK_TFLOPS,
+                "peak": peak,
+                "unit": unit,
+                "frac": achieved / peak,
                 "traffic": traffic,
                 "flops_per_problem_iter": F,
+                "bytes_per_problem_iter": Bq,
                 "problem_iters_per_launch": iters_per_launch,
             },
         }
         if not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
