@@ -78,8 +78,7 @@ enum : int {
   O_PART = O_CC + 12 * NCS,    // segment partials [NVMAX][NCS][2 slots] (zero where unused)
   O_TOTC = O_PART + 4 * NCS * 2,  // per-cone results [2][NCS]
   O_STAMPS = O_TOTC + 2 * NCS,  // diagnostic build: per-phase cycle totals of this wave [16]
-  O_KV = O_STAMPS + 16,        // 16 k-vectors of KMAX
-  O_FIXED_END = O_KV + 16 * KMAX
+  O_KV = O_STAMPS + 16         // 16 k-vectors, Shape::KS apart
 };
 // per-cone constants (SOC cones), recomputed by every scaling:
 //   MU = mu, IMU = 1/mu, WB0 = wbar_0, I1 = 1/(1+wbar_0), W2 = |wbar_1|^2,
@@ -92,15 +91,20 @@ __host__ __device__ constexpr int cc(int q, int c) { return O_CC + q * NCS + c; 
 // k-vector ids
 enum : int { KV_H, KV_Z, KV_S, KV_DZ, KV_DS, KV_RZ, KV_RS, KV_LAM, KV_WB, KV_CA, KV_CB, KV_K0,
              KV_K1, KV_K2, KV_T1, KV_T2 };
-__host__ __device__ constexpr int kv(int id) { return O_KV + id * KMAX; }
 
 template <int NQ, int NP, int MQ>
 struct Shape {
   static constexpr int NPAD = 16 * NQ, KP = 4 * NP, MPAD = 16 * MQ, LDA = NPAD + 1;
+  // k-vector stride: a shape whose k-vectors fit slot 0 (KP <= 64) packs them
+  // KP apart (C1: 20 KiB of LDS per wave, so 8 waves fit a CU).  Lanes read
+  // slot 1 / padding elements i >= KP unconditionally and mask the values by
+  // their type code (3 = pad), so those reads may alias the next vector; every
+  // write is guarded by i < k or the code, and rows [k, KP) stay zero.
+  static constexpr int KS = KP > 64 ? KMAX : KP;
   // sweep gather buffer: pivot column of the diagonal tile [16] + pivot row of
   // every tile of the panel slab [16 per tile]
   static constexpr int CB = 16 + (NPAD > MPAD ? NPAD : MPAD);
-  static constexpr int O_A = O_FIXED_END;
+  static constexpr int O_A = O_KV + 16 * KS;
   static constexpr int O_NV = O_A + MPAD * LDA;    // n-vectors: c x rd rx n0 tn
   static constexpr int O_MV = O_NV + 6 * NPAD;     // m-vectors: b y rp ry m0 tm
   static constexpr int O_U = O_MV + 6 * MPAD;      // U[NCS][NPAD]
@@ -115,7 +119,8 @@ enum : int { MV_B, MV_Y, MV_RP, MV_RY, MV_M0, MV_TM };
 
 inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
   int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = NPAD + 1, CB = 16 + (NPAD > MPAD ? NPAD : MPAD);
-  int total = O_FIXED_END + MPAD * LDA + 6 * NPAD + 6 * MPAD + NCS * NPAD + 2 * CB + 16 * 17;
+  int KS = 4 * NP > 64 ? KMAX : 4 * NP;  // Shape::KS
+  int total = O_KV + 16 * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + NCS * NPAD + 2 * CB + 16 * 17;
   return (size_t)total * sizeof(double);
 }
 
@@ -370,10 +375,11 @@ struct Small {
                        RX = SH::nv(NV_RX), N0 = SH::nv(NV_N0), TN = SH::nv(NV_TN);
   static constexpr int B_ = SH::mv(MV_B), Y_ = SH::mv(MV_Y), RP = SH::mv(MV_RP),
                        RY = SH::mv(MV_RY), M0 = SH::mv(MV_M0);
-  static constexpr int H_ = kv(KV_H), Z_ = kv(KV_Z), S_ = kv(KV_S), DZ = kv(KV_DZ),
-                       DS = kv(KV_DS), RZ = kv(KV_RZ), RS = kv(KV_RS), LAM = kv(KV_LAM),
-                       WB = kv(KV_WB), CA = kv(KV_CA), CBV = kv(KV_CB), K0 = kv(KV_K0),
-                       K1 = kv(KV_K1), K2 = kv(KV_K2), T1 = kv(KV_T1), T2 = kv(KV_T2);
+  static constexpr int kvs(int id) { return O_KV + id * SH::KS; }
+  static constexpr int H_ = kvs(KV_H), Z_ = kvs(KV_Z), S_ = kvs(KV_S), DZ = kvs(KV_DZ),
+                       DS = kvs(KV_DS), RZ = kvs(KV_RZ), RS = kvs(KV_RS), LAM = kvs(KV_LAM),
+                       WB = kvs(KV_WB), CA = kvs(KV_CA), CBV = kvs(KV_CB), K0 = kvs(KV_K0),
+                       K1 = kvs(KV_K1), K2 = kvs(KV_K2), T1 = kvs(KV_T1), T2 = kvs(KV_T2);
 
   const SmallArgs& a;
   const int lane, g, cl;
@@ -478,7 +484,7 @@ struct Small {
     double av[AB];
 #pragma unroll
     for (int t = 0; t < AB; ++t) av[t] = (64 * t + lane < mn) ? Ap[64 * t + lane] : 0.0;
-    for (int e = lane; e < 16 * KMAX; e += 64) LDS(O_KV + e) = 0.0;
+    for (int e = lane; e < 16 * SH::KS; e += 64) LDS(O_KV + e) = 0.0;
     for (int e = lane; e < SH::O_COL - O_A; e += 64) LDS(O_A + e) = 0.0;
     SYNC();
     if (lane < n) LDS(C_ + lane) = cv;
