@@ -98,7 +98,8 @@ def main():
                          "reference's stopping rule, tol=1e-5 absolute, maxit=40, per-problem masking (§8(d)(ii))")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic summary (tools/pmc_traffic.py); default profiles/r01_pmc_traffic[_<config>].json")
     args = ap.parse_args()
 
     import torch
@@ -177,9 +178,11 @@ def main():
         else:
             achieved, peak, unit = F * iters_per_launch / (kms * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
         traffic = None
-        if os.path.exists(args.traffic_json):
+        tj_path = args.traffic_json or os.path.join(
+            HERE, "profiles", "r01_pmc_traffic.json" if cfg.name == "C2" else f"r01_pmc_traffic_{cfg.name.lower()}.json")
+        if os.path.exists(tj_path):
             try:
-                tj = json.load(open(args.traffic_json))
+                tj = json.load(open(tj_path))
                 if tj.get("config") == cfg.name and tj.get("batch") == B and tj.get("fixed_k") == K:
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
