@@ -271,6 +271,25 @@ def test_random_shapes_early_parity(oracle, seed):
         assert rel(g["x"][p * n:(p + 1) * n], r["x"][p * n:(p + 1) * n]) <= 1e-8, (n, m, k, cones, p)
 
 
+@pytest.mark.parametrize("n,m,k,cones", [
+    (3, 1, 5, [(0, 0, 2), (1, 2, 3)]),                     # KP = 8: k-vectors 8 apart in LDS
+    (30, 6, 47, [(0, 0, 7), (1, 7, 20), (1, 27, 20)]),     # KP = 48, one padding row
+    (40, 8, 62, [(1, 0, 31), (1, 31, 31)]),                # KP = 64, two padding rows
+    (48, 16, 64, [(0, 0, 16), (1, 16, 48)]),               # KP = 64 exactly: last shape packed KP apart
+    (48, 16, 65, [(0, 0, 17), (1, 17, 48)]),               # KP = 68: two slots, 128 apart
+])
+def test_kvector_stride_boundaries(oracle, n, m, k, cones):
+    """The register kernel packs its k-vectors KP apart when KP <= 64 (and 128
+    apart otherwise); shapes on both sides of the boundary match the oracle."""
+    B = 16
+    d = oracle.generate(cones, B, n, m, k, 4242 + k)
+    r = oracle.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"], params=oracle.Params(maxit=3, tol=0.0))
+    g = S.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"], None, maxit=3, tol=0.0)
+    assert (g["status"] == r["status"]).all(), (g["status"], r["status"])
+    for key, dim in (("x", n), ("z", k), ("s", k)):
+        assert rel(g[key], r[key]) <= 1e-8, (key, rel(g[key], r[key]))
+
+
 def test_lp_and_m0_edge_cases(oracle):
     # pure LP (one POC cone, explicit-inverse sensitive: SURVEY.md §0.6) and m = 0
     for cones, n, m, k in (([(0, 0, 40)], 20, 5, 40), ([(1, 0, 24)], 16, 0, 24)):
