@@ -857,12 +857,21 @@ struct Large {
         for (int t = 0; t < nb; ++t) rowv[t] = LV(buf + 64 * t + ln);
 #pragma unroll
         for (int q = 0; q < 8; ++q) colv[q] = LV(buf + P0 + rr + 8 * q);
-        // rank-1 update of every element, then the pivot column (block P, lane
-        // c: a select) and the pivot row (one register row of one wavefront)
+        // rank-1 update of every element as (col_i sqrt(r)) (row_j sqrt(r)): one
+        // FMA per element, and (i,j), (j,i) multiply the same two numbers, so the
+        // diagonal block stays exactly symmetric (r = 1/d > 0 whenever ok holds);
+        // then the pivot column (block P, lane c: a select) and the pivot row
+        // (one register row of one wavefront)
+        const double sr = sqrt(r);
+        double rsq[nb], csq[8];
+#pragma unroll
+        for (int t = 0; t < nb; ++t) rsq[t] = rowv[t] * sr;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) csq[q] = colv[q] * sr;
 #pragma unroll
         for (int q = 0; q < 8; ++q)
 #pragma unroll
-          for (int t = 0; t < nb; ++t) Z[q][t] = fma(-(colv[q] * rowv[t]), r, Z[q][t]);
+          for (int t = 0; t < nb; ++t) Z[q][t] = fma(-csq[q], rsq[t], Z[q][t]);
         const bool lc = ln == c;
 #pragma unroll
         for (int t = 0; t < nb; ++t)
