@@ -608,6 +608,61 @@ struct Large {
     }
   }
 
+  // The same Gram update in the transposed orientation: acc[a][b] (lane (g, cl),
+  // register r) holds block element (I0 + 16b + cl, J0 + 16a + g + 4r), so the
+  // column-major read-modify-write of the block is 128 contiguous bytes per
+  // 16 lanes (load_blkT / store_blkT) instead of 32 bytes over 16 columns.
+  // LO (diagonal block): tiles with b < a lie above the diagonal (skipped).
+  template <bool LO = false>
+  __device__ __forceinline__ void gram_blkT(d4 (&acc)[4][4], gcdbl* Y, int ld, int I0, int J0, int qs) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll 1
+    for (int k0 = 0; k0 < 64; k0 += 16) {
+      double av[4][4], bv[4][4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        gcdbl* row = Y + (int64_t)(k0 + 4 * s + g) * ld;
+        const double f = LV(qs + k0 + 4 * s + g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          av[t][s] = f * row[J0 + 16 * t + cl];
+          bv[t][s] = row[I0 + 16 * t + cl];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int a_ = 0; a_ < 4; ++a_)
+#pragma unroll
+          for (int b_ = 0; b_ < 4; ++b_)
+            if (!LO || b_ >= a_) acc[a_][b_] = mfma(av[a_][s], bv[b_][s], acc[a_][b_]);
+    }
+  }
+  template <bool LO = false>
+  __device__ __forceinline__ void load_blkT(d4 (&acc)[4][4], gcdbl* M, int ld, int I0, int J0) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int a_ = 0; a_ < 4; ++a_)
+#pragma unroll
+      for (int b_ = 0; b_ < 4; ++b_)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[a_][b_][r] = (LO && b_ < a_) ? 0.0 : M[(int64_t)(J0 + 16 * a_ + g + 4 * r) * ld + I0 + 16 * b_ + cl];
+  }
+  template <bool LO = false>
+  __device__ __forceinline__ void store_blkT(const d4 (&acc)[4][4], gdbl* M, int ld, int I0, int J0) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int a_ = 0; a_ < 4; ++a_)
+#pragma unroll
+      for (int b_ = 0; b_ < 4; ++b_)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (LO && b_ < a_) continue;
+          M[(int64_t)(J0 + 16 * a_ + g + 4 * r) * ld + I0 + 16 * b_ + cl] = acc[a_][b_][r];
+        }
+  }
+
   // 64x64 block (I0, J0) of a column-major matrix <-> the f64 MFMA C/D layout
   // (lane (g, cl) holds rows g + 4r, column cl of each 16x16 tile)
   template <bool LO = false>
@@ -912,13 +967,13 @@ struct Large {
         const int I = a_ + (a_ >= P ? 1 : 0), J = b_ + (b_ >= P ? 1 : 0);
         d4 acc[4][4];
         if (I == J) {
-          load_blk<true>(acc, M, ld, 64 * I, 64 * J);
-          gram_blk<true>(acc, Y, RW, 64 * I, 64 * J, o_rv);
-          store_blk<true>(acc, M, ld, 64 * I, 64 * J, NOPAD);
+          load_blkT<true>(acc, M, ld, 64 * I, 64 * J);
+          gram_blkT<true>(acc, Y, RW, 64 * I, 64 * J, o_rv);
+          store_blkT<true>(acc, M, ld, 64 * I, 64 * J);
         } else {
-          load_blk(acc, M, ld, 64 * I, 64 * J);
-          gram_blk(acc, Y, RW, 64 * I, 64 * J, o_rv);
-          store_blk(acc, M, ld, 64 * I, 64 * J, NOPAD);
+          load_blkT(acc, M, ld, 64 * I, 64 * J);
+          gram_blkT(acc, Y, RW, 64 * I, 64 * J, o_rv);
+          store_blkT(acc, M, ld, 64 * I, 64 * J);
         }
       }
       BAR();
