@@ -1,0 +1,100 @@
+"""Committed oracle trajectories (tests/golden/trajectories.json, made by
+tests/golden/make_trajectories.py; SURVEY.md §8(c) "Fixtures to commit").
+
+CPU: the oracle still reproduces every committed iterate (a regression pin on
+the restatement itself).  GPU: the HIP path's iterates match the committed ones
+for as long as every dense KKT system on the way had kappa_2(H) <= 1e5 (the
+window SURVEY.md §8(c) asserts parity in), within
+rel <= max(1e-8, 1e-12 * max_j kappa_2(H_j)): P4's 1e-8 while the systems are
+well conditioned, growing with the worst conditioning met on the way (the
+tiny runtests.jl problems reach kappa ~ 2e4 by their fourth iterate).  The
+first 3 (C1) / 6 (C2) iterations are also held to 1e-8 against the live
+oracle in test_gpu_parity.py::test_trajectory_parity."""
+import base64
+import json
+import os
+
+import numpy as np
+import pytest
+
+from problems import kat_problem
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KAPPA_MAX = 1e5
+
+
+def _arr(s):
+    return np.frombuffer(base64.b64decode(s), dtype="<f8")
+
+
+@pytest.fixture(scope="module")
+def fixture():
+    with open(os.path.join(HERE, "golden", "trajectories.json")) as f:
+        return json.load(f)
+
+
+def _problem(case, kats, oracle):
+    src = case["source"]
+    if "kats" in src:
+        cones, c, A, b, G, h = kat_problem(kats[src["kats"]])
+        return cones, c, np.asarray(A).reshape(-1, len(c)), b, G, h
+    from socp_amd.configs import CONFIGS
+    cfg = CONFIGS[src["config"]]
+    p = src["problem"]
+    d = oracle.generate(cfg.cones, p + 1, cfg.n, cfg.m, cfg.k, src["seed"])
+    n, m, k = cfg.n, cfg.m, cfg.k
+    return ([tuple(t) for t in cfg.cones], d["c"][p * n:(p + 1) * n],
+            d["A"][p * m * n:(p + 1) * m * n].reshape(n, m).T, d["b"][p * m:(p + 1) * m],
+            d["G"][p * k * n:(p + 1) * k * n].reshape(n, k).T, d["h"][p * k:(p + 1) * k])
+
+
+def _rel(a, b):
+    nb = np.linalg.norm(b)
+    return np.linalg.norm(a - b) / (nb if nb > 0 else 1.0)
+
+
+def test_fixture_shape(fixture):
+    names = [c["name"] for c in fixture["cases"]]
+    assert {"soc1", "soc2", "soc3"} <= set(names)
+    assert sum(n.startswith("C2#") for n in names) >= 4 and sum(n.startswith("C1#") for n in names) >= 8
+    for c in fixture["cases"]:
+        for it in c["iterates"]:
+            assert len(_arr(it["x"])) == c["n"] and len(_arr(it["z"])) == c["k"] and len(_arr(it["s"])) == c["k"]
+
+
+def test_oracle_reproduces_fixture(fixture, kats, oracle):
+    for case in fixture["cases"]:
+        cones, c, A, b, G, h = _problem(case, kats, oracle)
+        T = len(case["iterates"]) - 1
+        r = oracle.solve_trace(cones, c, A, b, G, h, params=oracle.Params(maxit=T, tol=0.0))
+        states = list(r["trace"][:r["iters"]]) + [(r["x"], r["y"], r["z"], r["s"])]
+        assert len(states) == T + 1, case["name"]
+        for t, (it, st) in enumerate(zip(case["iterates"], states)):
+            for key, v in zip("xzs", (st[0], st[2], st[3])):
+                assert _rel(v, _arr(it[key])) <= 1e-12, (case["name"], t, key)
+
+
+@pytest.mark.gpu
+def test_hip_trajectories_match_fixture(fixture, kats, oracle):
+    import socp_amd as S
+    checked = 0
+    for case in fixture["cases"]:
+        cones, c, A, b, G, h = _problem(case, kats, oracle)
+        n, m, k = case["n"], case["m"], case["k"]
+        kap = [it["kappa_H"] for it in case["iterates"]]
+        Af = np.asarray(A, dtype=np.float64).reshape(m, n).ravel(order="F") if m else None
+        Gf = np.asarray(G, dtype=np.float64).ravel(order="F")
+        sing = np.array([case["sing"]], np.uint8)
+        for t in range(1, len(case["iterates"])):
+            if any(x is None or x > KAPPA_MAX for x in kap[:t]):
+                break
+            tol = max(1e-8, 1e-12 * max(kap[:t]))
+            g = S.batch_solve(cones, n, m, k, np.asarray(c, float), Af, np.asarray(b, float) if m else None,
+                              Gf, np.asarray(h, float), sing, maxit=t, tol=0.0)
+            assert int(g["status"][0]) == S.MAXIT, (case["name"], t)
+            it = case["iterates"][t]
+            for key in "xzs":
+                e = _rel(g[key], _arr(it[key]))
+                assert e <= tol, (case["name"], t, key, e, tol)
+            checked += 1
+    assert checked >= 40, checked
