@@ -579,36 +579,9 @@ struct Large {
     }
   }
 
-  // acc[ta][tb] += sum_{c<64} Y[c][I0+16ta+i] * (LDS[qs+c] * Y[c][J0+16tb+j]) for the
-  // row-major 64-row panel Y (row c at Y + c*ld): the sweep's deferred Gram update.
-  // At MFMA step s, lane group g feeds row k0 + 4s + g (C/D row order).
-  template <bool LO = false>
-  __device__ __forceinline__ void gram_blk(d4 (&acc)[4][4], gcdbl* Y, int ld, int I0, int J0, int qs) {
-    const int g = lane >> 4, cl = lane & 15;
-#pragma unroll 1
-    for (int k0 = 0; k0 < 64; k0 += 16) {
-      double av[4][4], bv[4][4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        gcdbl* row = Y + (int64_t)(k0 + 4 * s + g) * ld;
-        const double f = LV(qs + k0 + 4 * s + g);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          av[t][s] = row[I0 + 16 * t + cl];
-          bv[t][s] = f * row[J0 + 16 * t + cl];
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int ta = 0; ta < 4; ++ta)
-#pragma unroll
-          for (int tb = 0; tb < 4; ++tb)
-            if (!LO || tb <= ta) acc[ta][tb] = mfma(av[ta][s], bv[tb][s], acc[ta][tb]);
-    }
-  }
-
-  // The same Gram update in the transposed orientation: acc[a][b] (lane (g, cl),
+  // The sweep's deferred Gram update, acc += sum_{c<64} Y[c][I-slice]' (LDS[qs+c]
+  // Y[c][J-slice]) for the row-major 64-row panel Y (row c at Y + c*ld), in the
+  // transposed MFMA orientation: acc[a][b] (lane (g, cl),
   // register r) holds block element (I0 + 16b + cl, J0 + 16a + g + 4r), so the
   // column-major read-modify-write of the block is 128 contiguous bytes per
   // 16 lanes (load_blkT / store_blkT) instead of 32 bytes over 16 columns.
