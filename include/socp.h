@@ -172,6 +172,28 @@ int socp_pack_csc(socp_ctx* ctx, int64_t batch, int32_t rows, int32_t cols,
                   const int64_t* nz_offs, const int64_t* colptr, const int64_t* rowval,
                   const double* nzval, int32_t index_base, double* dense);
 
+/* Multi-GPU outcome gather: problems shard across ranks
+ * (one process per GPU) with no data-path exchange; the only collective is the
+ * all-gather of each problem's (status, iters) over RCCL (xGMI between the
+ * GPUs of a node).  This replaces nothing in the reference (which solves one
+ * problem per call, solver.jl:40); it is the exchange step of the batched
+ * multi-GPU drop-in.  RCCL (librccl.so.1) is opened on first use, so the rest
+ * of the library has no RCCL dependency.
+ *   rank 0: socp_comm_unique_id(id), then hands the 128 bytes to every rank
+ *           (MPI broadcast, a file, torch.distributed ...);
+ *   every rank: socp_comm_init(ctx, nranks, rank, id, &comm);
+ *   socp_allgather_status(comm, B, status, iters, out): device pointers;
+ *           out[(r*B + p)*2 + 0] = status, [.. + 1] = iters of rank r's
+ *           problem p; equal B on every rank; stream-ordered on the
+ *           context's stream (socp_ctx_sync to wait). */
+#define SOCP_COMM_ID_BYTES 128
+typedef struct socp_comm socp_comm;
+int socp_comm_unique_id(unsigned char* id);
+int socp_comm_init(socp_ctx* ctx, int nranks, int rank, const unsigned char* id, socp_comm** out);
+int socp_comm_destroy(socp_comm* comm);
+int socp_allgather_status(socp_comm* comm, int64_t batch, const int32_t* status, const int32_t* iters,
+                          int32_t* out);
+
 /* Timing of the last solve's main kernel, measured with HIP events on the
  * context's stream (milliseconds), and its name. */
 int socp_last_kernel_ms(socp_ctx* ctx, float* ms);

@@ -2,7 +2,9 @@
 // variant dispatch for the register-resident solver kernel, the device-side
 // problem generator.  Host pointers are staged through context-owned device
 // buffers; device pointers (SOCP_F_DEVICE_PTRS) are used in place.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -663,5 +665,118 @@ extern "C" int socp_pack_csc(socp_ctx* ctx, int64_t batch, int32_t rows, int32_t
   HIPCHK(hipStreamSynchronize(ctx->stream));
   if (herr & 1) return fail(SOCP_E_INVALID, "colptr does not span the problem's nonzeros");
   if (herr & 2) return fail(SOCP_E_INVALID, "row index out of range");
+  return 0;
+}
+
+// ------------------------------------------------------------ multi-GPU gather
+// RCCL entry points resolved from librccl.so.1 on first use (a process that
+// already loaded it, e.g. through torch, shares that copy: same soname).
+namespace {
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclGetErrorString) err_str = nullptr;
+  bool ok = false;
+};
+const Rccl* rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    r.get_id = (decltype(r.get_id))dlsym(h, "ncclGetUniqueId");
+    r.init_rank = (decltype(r.init_rank))dlsym(h, "ncclCommInitRank");
+    r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+    r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+    r.err_str = (decltype(r.err_str))dlsym(h, "ncclGetErrorString");
+    r.ok = r.get_id && r.init_rank && r.destroy && r.all_gather && r.err_str;
+  });
+  return r.ok ? &r : nullptr;
+}
+
+__global__ void socp_pair_kernel(int64_t B, const int32_t* __restrict__ status, const int32_t* __restrict__ iters,
+                                 int32_t* __restrict__ pairs) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < B) {
+    pairs[2 * p] = status[p];
+    pairs[2 * p + 1] = iters[p];
+  }
+}
+}  // namespace
+
+struct socp_comm {
+  socp_ctx* ctx = nullptr;
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0;
+  DevBuf pairs;
+};
+
+static_assert(sizeof(ncclUniqueId) == SOCP_COMM_ID_BYTES, "ncclUniqueId size");
+
+#define RCCLCHK(R, x)                                                                       \
+  do {                                                                                     \
+    ncclResult_t r_ = (x);                                                                 \
+    if (r_ != ncclSuccess) return fail(SOCP_E_HIP, std::string(#x) + ": " + (R)->err_str(r_)); \
+  } while (0)
+
+extern "C" int socp_comm_unique_id(unsigned char* id) {
+  if (!id) return fail(SOCP_E_INVALID, "id is NULL");
+  const Rccl* R = rccl();
+  if (!R) return fail(SOCP_E_UNSUPPORTED, "librccl.so.1 not found");
+  ncclUniqueId u;
+  RCCLCHK(R, R->get_id(&u));
+  memcpy(id, &u, sizeof(u));
+  return 0;
+}
+
+extern "C" int socp_comm_init(socp_ctx* ctx, int nranks, int rank, const unsigned char* id, socp_comm** out) {
+  if (!ctx || !id || !out) return fail(SOCP_E_INVALID, "NULL argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(SOCP_E_INVALID, "bad nranks/rank");
+  const Rccl* R = rccl();
+  if (!R) return fail(SOCP_E_UNSUPPORTED, "librccl.so.1 not found");
+  HIPCHK(hipSetDevice(ctx->device));
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  auto* c = new socp_comm();
+  c->ctx = ctx;
+  c->nranks = nranks;
+  c->rank = rank;
+  const ncclResult_t r = R->init_rank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail(SOCP_E_HIP, std::string("ncclCommInitRank: ") + R->err_str(r));
+  }
+  *out = c;
+  return 0;
+}
+
+extern "C" int socp_comm_destroy(socp_comm* comm) {
+  if (!comm) return 0;
+  const Rccl* R = rccl();
+  if (R && comm->comm) (void)R->destroy(comm->comm);
+  (void)hipSetDevice(comm->ctx->device);
+  comm->pairs.release();
+  delete comm;
+  return 0;
+}
+
+extern "C" int socp_allgather_status(socp_comm* comm, int64_t batch, const int32_t* status, const int32_t* iters,
+                                     int32_t* out) {
+  if (!comm) return fail(SOCP_E_INVALID, "comm is NULL");
+  if (batch < 0) return fail(SOCP_E_INVALID, "negative batch");
+  if (batch == 0) return 0;
+  if (!status || !iters || !out) return fail(SOCP_E_INVALID, "NULL pointer");
+  const Rccl* R = rccl();
+  socp_ctx* ctx = comm->ctx;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (comm->pairs.ensure((size_t)batch * 2 * sizeof(int32_t))) return fail(SOCP_E_NOMEM, "device allocation failed");
+  int32_t* pairs = (int32_t*)comm->pairs.p;
+  hipLaunchKernelGGL(socp_pair_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, ctx->stream, batch,
+                     status, iters, pairs);
+  HIPCHK(hipGetLastError());
+  RCCLCHK(R, R->all_gather(pairs, out, (size_t)batch * 2, ncclInt32, comm->comm, ctx->stream));
   return 0;
 }

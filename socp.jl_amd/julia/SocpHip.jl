@@ -141,3 +141,40 @@ function solve_socp_batched(problems::AbstractVector{<:Problem}; maxit=40, tol=1
               for i in 1:B]
     return states, iters, status
 end
+
+# ------------------------------------------------------- multi-GPU gather
+# One process per GPU (e.g. under MPI.jl); problems shard by contiguous global
+# index and the only collective is the RCCL all-gather of (status, iters)
+# (include/socp.h: socp_comm_*, socp_allgather_status).  Rank 0 makes the id,
+# the host broadcasts it (MPI.Bcast! below is the usual way).
+const SOCP_COMM_ID_BYTES = 128
+
+function socp_comm_unique_id()
+    id = zeros(UInt8, SOCP_COMM_ID_BYTES)
+    socp_check(ccall((:socp_comm_unique_id, libsocp), Cint, (Ptr{UInt8},), id))
+    return id
+end
+
+function socp_comm_init(nranks::Integer, rank::Integer, id::Vector{UInt8})
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    socp_check(ccall((:socp_comm_init, libsocp), Cint,
+                     (Ptr{Cvoid}, Cint, Cint, Ptr{UInt8}, Ptr{Ptr{Cvoid}}),
+                     socp_ctx(), nranks, rank, id, h))
+    return h[]
+end
+
+socp_comm_destroy(comm::Ptr{Cvoid}) = ccall((:socp_comm_destroy, libsocp), Cint, (Ptr{Cvoid},), comm)
+
+# status, iters, out: device pointers (out holds nranks * B * 2 Int32, rank-major)
+function socp_allgather_status(comm::Ptr{Cvoid}, B::Integer, status::Ptr{Int32}, iters::Ptr{Int32},
+                               out::Ptr{Int32})
+    socp_check(ccall((:socp_allgather_status, libsocp), Cint,
+                     (Ptr{Cvoid}, Int64, Ptr{Int32}, Ptr{Int32}, Ptr{Int32}), comm, B, status, iters, out))
+    socp_check(ccall((:socp_ctx_sync, libsocp), Cint, (Ptr{Cvoid},), socp_ctx()))
+    return nothing
+end
+
+# Example (MPI.jl):
+#   id = MPI.Comm_rank(comm) == 0 ? socp_comm_unique_id() : zeros(UInt8, SOCP_COMM_ID_BYTES)
+#   MPI.Bcast!(id, 0, comm)
+#   c = socp_comm_init(MPI.Comm_size(comm), MPI.Comm_rank(comm), id)

@@ -25,7 +25,8 @@ EXPORTED = [
     "socp_ctx_destroy", "socp_ctx_sync", "socp_ctx_stream", "socp_supported",
     "socp_batch_solve", "socp_batch_solve_ex", "socp_batch_kkt_solve", "socp_generate",
     "socp_last_kernel_ms", "socp_last_kernel_name", "socp_debug_set_kkt_dump",
-    "socp_debug_set_stamps", "socp_pack_csc",
+    "socp_debug_set_stamps", "socp_pack_csc", "socp_comm_unique_id", "socp_comm_init",
+    "socp_comm_destroy", "socp_allgather_status",
 ]
 
 
@@ -94,6 +95,10 @@ def load():
     L.socp_debug_set_kkt_dump.argtypes = [vp]
     L.socp_debug_set_stamps.argtypes = [vp]
     L.socp_pack_csc.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_int32, vp]
+    L.socp_comm_unique_id.argtypes = [vp]
+    L.socp_comm_init.argtypes = [vp, C.c_int, C.c_int, vp, C.POINTER(C.c_void_p)]
+    L.socp_comm_destroy.argtypes = [vp]
+    L.socp_allgather_status.argtypes = [vp, C.c_int64, vp, vp, vp]
     _lib = L
     return L
 

@@ -23,3 +23,49 @@ def gather_outcomes(status, iters, group=None):
     out = torch.empty((world,) + tuple(local.shape), dtype=torch.int32, device=local.device)
     dist.all_gather_into_tensor(out.view(-1, 2), local, group=group)
     return out
+
+
+COMM_ID_BYTES = 128  # SOCP_COMM_ID_BYTES (include/socp.h)
+
+
+class StatusComm:
+    """The C-ABI RCCL gather (socp_comm_* / socp_allgather_status, include/socp.h):
+    what a non-Python host (the Julia shim) uses instead of torch.distributed.
+    `uid` is the 128-byte id from `unique_id()` on rank 0, distributed by the host."""
+
+    def __init__(self, ctx, nranks: int, rank: int, uid: bytes):
+        import ctypes as C
+        from . import _lib
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("uid must be 128 bytes")
+        self._L = _lib.load()
+        self.ctx, self.nranks, self.rank = ctx, nranks, rank
+        self._uid = C.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        h = C.c_void_p()
+        _lib.check(self._L.socp_comm_init(ctx.handle, nranks, rank, self._uid, C.byref(h)))
+        self.handle = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+        from . import _lib
+        buf = C.create_string_buffer(COMM_ID_BYTES)
+        _lib.check(_lib.load().socp_comm_unique_id(buf))
+        return buf.raw
+
+    def allgather_status(self, status, iters):
+        """int32 [nranks, B, 2] of every rank's (status, iters); device tensors in and out."""
+        import torch
+        from . import _lib
+        B = status.numel()
+        out = torch.empty((self.nranks, B, 2), dtype=torch.int32, device=status.device)
+        st = status.to(torch.int32).contiguous()
+        it = iters.to(torch.int32).contiguous()
+        _lib.check(self._L.socp_allgather_status(self.handle, B, _lib.ptr(st), _lib.ptr(it), _lib.ptr(out)))
+        self.ctx.sync()
+        return out
+
+    def close(self):
+        if self.handle:
+            self._L.socp_comm_destroy(self.handle)
+            self.handle = None

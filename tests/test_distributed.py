@@ -72,3 +72,27 @@ def test_gloo_world2_matches_single_process(oracle):
                            params=oracle.Params(maxit=40, tol=1e-5), nthreads=1)
     flat = got.reshape(total, 2)
     assert np.array_equal(flat[:, 0], r["status"]) and np.array_equal(flat[:, 1], r["iters"])
+
+
+@pytest.mark.gpu
+def test_abi_status_gather_single_rank():
+    """socp_comm_* / socp_allgather_status (the C-ABI RCCL gather a Julia host
+    uses) on a one-rank communicator: the output is every rank's interleaved
+    (status, iters).  More ranks need more GPUs than a test box has; the
+    torch.distributed path of bench.py covers N > 1."""
+    import torch
+    import socp_amd as S
+    from socp_amd.dist import StatusComm
+    ctx = S.default_context()
+    uid = StatusComm.unique_id()
+    assert len(uid) == 128
+    comm = StatusComm(ctx, 1, 0, uid)
+    try:
+        B = 1000
+        st = torch.randint(0, 5, (B,), dtype=torch.int32, device="cuda")
+        it = torch.randint(0, 41, (B,), dtype=torch.int32, device="cuda")
+        out = comm.allgather_status(st, it)
+        assert out.shape == (1, B, 2)
+        assert torch.equal(out[0, :, 0], st) and torch.equal(out[0, :, 1], it)
+    finally:
+        comm.close()
