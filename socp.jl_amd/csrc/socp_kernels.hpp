@@ -26,7 +26,7 @@ struct LargeLayout {
   // LDS offsets (doubles)
   int o_rc, o_cc, o_kv, o_nv, o_mv, o_row, o_rv, o_part, o_red, o_fx, total;
   // workspace-slot offsets (doubles)
-  int64_t w_x, w_h, w_ap, w_at, w_yp, w_t, w_s, w_total;
+  int64_t w_x, w_h, w_ap, w_at, w_yp, w_rv, w_t, w_s, w_total;
 };
 __host__ __device__ inline int64_t large_al(int64_t v) { return (v + 31) / 32 * 32; }
 __host__ __device__ inline LargeLayout large_layout(int n, int m, int k) {
@@ -52,7 +52,8 @@ __host__ __device__ inline LargeLayout large_layout(int n, int m, int k) {
   L.w_h = w;  w += large_al((int64_t)L.NPAD * L.NPAD);  // H -> Li
   L.w_ap = w; w += large_al((int64_t)L.MPAD * L.NPAD);  // A, column-major
   L.w_at = w; w += large_al((int64_t)L.NPAD * L.MPAD);  // A, row-major
-  L.w_yp = w; w += large_al((int64_t)64 * L.RW);        // sweep pivot rows
+  L.w_yp = w; w += large_al((int64_t)L.RW * L.RW);      // sweep pivot rows, 64 x RW per panel
+  L.w_rv = w; w += large_al((int64_t)L.RW);             // sweep: -1/d of every pivot
   L.w_t = w;  w += large_al((int64_t)L.NPAD * L.MPAD);  // Li A'
   L.w_s = w;  w += large_al((int64_t)L.MPAD * L.MPAD);  // S -> S^-1
   L.w_total = w;

@@ -90,7 +90,7 @@ struct Large {
   int kpoc, csoc;  // POC elements (POC cones come first) and index of the first SOC cone
   bool sing;
   gcdbl* Gp;
-  gdbl *Xw, *Hm, *Ap, *At, *Yp, *Tm, *Sm;
+  gdbl *Xw, *Hm, *Ap, *At, *Yp, *Rv, *Tm, *Sm;
   // LDS vector offsets (doubles)
   int H_, Z_, S_, DZ, DS, RZ, RS, LAM, WB, CA, K0, K1, K2, T1, T2;
   int C_, X_, RD, RX, N0, TN;
@@ -107,6 +107,7 @@ struct Large {
     Ap = ws + L.w_ap;
     At = ws + L.w_at;
     Yp = ws + L.w_yp;
+    Rv = ws + L.w_rv;
     Tm = ws + L.w_t;
     Sm = ws + L.w_s;
     const int kv = L.o_kv, KP = L.KP;
@@ -579,7 +580,7 @@ struct Large {
     }
   }
 
-  // The sweep's deferred Gram update, acc += sum_{c<64} Y[c][I-slice]' (LDS[qs+c]
+  // The sweep's deferred Gram update, acc += sum_{c<64} Y[c][I-slice]' (fv[c]
   // Y[c][J-slice]) for the row-major 64-row panel Y (row c at Y + c*ld), in the
   // transposed MFMA orientation: acc[a][b] (lane (g, cl),
   // register r) holds block element (I0 + 16b + cl, J0 + 16a + g + 4r), so the
@@ -587,7 +588,7 @@ struct Large {
   // 16 lanes (load_blkT / store_blkT) instead of 32 bytes over 16 columns.
   // LO (diagonal block): tiles with b < a lie above the diagonal (skipped).
   template <bool LO = false>
-  __device__ __forceinline__ void gram_blkT(d4 (&acc)[4][4], gcdbl* Y, int ld, int I0, int J0, int qs) {
+  __device__ __forceinline__ void gram_blkT(d4 (&acc)[4][4], gcdbl* Y, int ld, int I0, int J0, gcdbl* fv) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll 1
     for (int k0 = 0; k0 < 64; k0 += 16) {
@@ -595,7 +596,7 @@ struct Large {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         gcdbl* row = Y + (int64_t)(k0 + 4 * s + g) * ld;
-        const double f = LV(qs + k0 + 4 * s + g);
+        const double f = fv[k0 + 4 * s + g];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           av[t][s] = f * row[J0 + 16 * t + cl];
@@ -845,10 +846,32 @@ struct Large {
     // members copied to locals: the step loop has a barrier in it, after which
     // members (this is a stack object once sweep is an out-of-line call) would
     // be reloaded from scratch
-    const int rr = wv, ln = lane, t0 = tid, o_row = L.o_row, RW = L.RW, o_rv = L.o_rv;
-    gdbl* const Y = Yp;
+    const int rr = wv, ln = lane, t0 = tid, o_row = L.o_row, RW = L.RW;
     for (int P = 0; P < nb; ++P) {
       const int P0 = 64 * P;
+      gdbl* const Y = Yp + (int64_t)P * 64 * RW;  // this panel's pivot rows
+      gdbl* const rv = Rv + P0;                    // and -1/d of its pivots
+      // Catch-up of row block P: its blocks receive the Gram updates of the
+      // earlier panels they have not seen (block (t, P), t >= P: panels [0, P);
+      // block (P, t), t < P: panels (t, P) -- panel t swept it as part of row t)
+      for (int t = rr; t < nb; t += NW) {
+        const int I = t > P ? t : P, J = t > P ? P : t;
+        const int qlo = t < P ? t + 1 : 0;
+        if (qlo >= P) continue;
+        d4 acc[4][4];
+        if (I == J) {
+          load_blkT<true>(acc, M, ld, 64 * I, 64 * J);
+          for (int Q = qlo; Q < P; ++Q)
+            gram_blkT<true>(acc, Yp + (int64_t)Q * 64 * RW, RW, 64 * I, 64 * J, Rv + 64 * Q);
+          store_blkT<true>(acc, M, ld, 64 * I, 64 * J);
+        } else {
+          load_blkT(acc, M, ld, 64 * I, 64 * J);
+          for (int Q = qlo; Q < P; ++Q)
+            gram_blkT(acc, Yp + (int64_t)Q * 64 * RW, RW, 64 * I, 64 * J, Rv + 64 * Q);
+          store_blkT(acc, M, ld, 64 * I, 64 * J);
+        }
+      }
+      BAR();
       double Z[8][nb];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -879,7 +902,7 @@ struct Large {
         const double d = LV(buf + P0 + c);
         ok = ok && (d > 0.0);
         const double r = 1.0 / d;
-        if (t0 == 0) LV(o_rv + c) = -r;
+        if (t0 == 0) rv[c] = -r;
         double rowv[nb], colv[8];
 #pragma unroll
         for (int t = 0; t < nb; ++t) rowv[t] = LV(buf + 64 * t + ln);
@@ -933,24 +956,31 @@ struct Large {
           }
         }
       }
-      const int no = nb - 1, ng = no * (no + 1) / 2;
-      for (int t = rr; t < ng; t += NW) {
-        int a_, b_;
-        tri_ij(t, a_, b_);
-        const int I = a_ + (a_ >= P ? 1 : 0), J = b_ + (b_ >= P ? 1 : 0);
-        d4 acc[4][4];
-        if (I == J) {
-          load_blkT<true>(acc, M, ld, 64 * I, 64 * J);
-          gram_blkT<true>(acc, Y, RW, 64 * I, 64 * J, o_rv);
-          store_blkT<true>(acc, M, ld, 64 * I, 64 * J);
-        } else {
-          load_blkT(acc, M, ld, 64 * I, 64 * J);
-          gram_blkT(acc, Y, RW, 64 * I, 64 * J, o_rv);
-          store_blkT(acc, M, ld, 64 * I, 64 * J);
-        }
-      }
-      BAR();
+      BAR();  // panel P written back before the next catch-up reads its neighbours
     }
+    // Final catch-up: block (I, J), I >= J, has seen the panels up to I; it
+    // receives those after I.  Each block is thus read and written 3 times per
+    // sweep instead of once per panel; the Gram products (and their order) are
+    // the right-looking sweep's, so the result is the same to the bit.
+    const int ng = nb * (nb + 1) / 2;
+    for (int t = rr; t < ng; t += NW) {
+      int I, J;
+      tri_ij(t, I, J);
+      if (I + 1 >= nb) continue;
+      d4 acc[4][4];
+      if (I == J) {
+        load_blkT<true>(acc, M, ld, 64 * I, 64 * J);
+        for (int Q = I + 1; Q < nb; ++Q)
+          gram_blkT<true>(acc, Yp + (int64_t)Q * 64 * RW, RW, 64 * I, 64 * J, Rv + 64 * Q);
+        store_blkT<true>(acc, M, ld, 64 * I, 64 * J);
+      } else {
+        load_blkT(acc, M, ld, 64 * I, 64 * J);
+        for (int Q = I + 1; Q < nb; ++Q)
+          gram_blkT(acc, Yp + (int64_t)Q * 64 * RW, RW, 64 * I, 64 * J, Rv + 64 * Q);
+        store_blkT(acc, M, ld, 64 * I, 64 * J);
+      }
+    }
+    BAR();
     return true;
   }
 
