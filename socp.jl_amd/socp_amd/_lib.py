@@ -95,10 +95,11 @@ def load():
     L.socp_debug_set_kkt_dump.argtypes = [vp]
     L.socp_debug_set_stamps.argtypes = [vp]
     L.socp_pack_csc.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_int32, vp]
-    L.socp_comm_unique_id.argtypes = [vp]
-    L.socp_comm_init.argtypes = [vp, C.c_int, C.c_int, vp, C.POINTER(C.c_void_p)]
-    L.socp_comm_destroy.argtypes = [vp]
-    L.socp_allgather_status.argtypes = [vp, C.c_int64, vp, vp, vp]
+    if hasattr(L, "socp_comm_init"):  # RCCL gather (absent from libraries built before it)
+        L.socp_comm_unique_id.argtypes = [vp]
+        L.socp_comm_init.argtypes = [vp, C.c_int, C.c_int, vp, C.POINTER(C.c_void_p)]
+        L.socp_comm_destroy.argtypes = [vp]
+        L.socp_allgather_status.argtypes = [vp, C.c_int64, vp, vp, vp]
     _lib = L
     return L
 
