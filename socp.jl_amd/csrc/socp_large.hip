@@ -1000,13 +1000,33 @@ struct Large {
   }
 
   // M (lower triangle = -X^-1) -> X^-1 in both triangles
+  // by 64x64 lower blocks in the transposed MFMA orientation: the block is
+  // read and rewritten in 128-byte rows, its mirror written in 32-byte runs
+  // (element-wise mirroring wrote 8 bytes per cache line)
   __device__ void finalize_sym(gdbl* M, int ld) {
-    for (int C = wv; C < ld; C += NW)
-      for (int R = C + lane; R < ld; R += 64) {
-        const double v = -M[(int64_t)C * ld + R];
-        M[(int64_t)C * ld + R] = v;
-        if (R != C) M[(int64_t)R * ld + C] = v;
-      }
+    const int NB = ld / 64, g = lane >> 4, cl = lane & 15;
+    for (int t = wv; t < NB * (NB + 1) / 2; t += NW) {
+      int I, J;
+      tri_ij(t, I, J);
+      d4 acc[4][4];
+      if (I == J)
+        load_blkT<true>(acc, M, ld, 64 * I, 64 * J);
+      else
+        load_blkT(acc, M, ld, 64 * I, 64 * J);
+#pragma unroll
+      for (int a_ = 0; a_ < 4; ++a_)
+#pragma unroll
+        for (int b_ = 0; b_ < 4; ++b_)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (I == J && b_ < a_) continue;
+            const int i = 64 * I + 16 * b_ + cl, j = 64 * J + 16 * a_ + g + 4 * r;
+            if (i < j) continue;  // upper half of a diagonal tile: not maintained
+            const double v = -acc[a_][b_][r];
+            M[(int64_t)j * ld + i] = v;
+            if (i != j) M[(int64_t)i * ld + j] = v;
+          }
+    }
     BAR();
   }
 

@@ -9,6 +9,6 @@ Y=$PWD/socp.jl_amd/lib_y/libsocp.so
 for rep in 1 2 3; do
   for lib in "" "$Y"; do
     SOCP_AMD_LIB=$lib timeout -k 10 200 python bench.py --config C4 --no-cpu --steps 3 --warmup 1 > gpurun_out/abi.log 2>&1 || { tail -20 gpurun_out/abi.log; exit 1; }
-    python -c "import json; d=json.loads(open('gpurun_out/abi.log').read().strip().splitlines()[-1]); print('${lib:+old }${lib:-new}'.split()[0], round(d['kernel_ms'], 2))"
+    python -c "import json; d=json.loads(open('gpurun_out/abi.log').read().strip().splitlines()[-1]); print('${lib:+B }${lib:-A}'.split()[0], round(d['kernel_ms'], 2))"
   done
 done
