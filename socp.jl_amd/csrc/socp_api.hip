@@ -19,6 +19,9 @@
 using namespace socp;
 
 static thread_local std::string g_err;
+// the persistent kernels pull problem indices from an int32 counter and the
+// per-problem launches use one workgroup per problem (grid.x)
+static constexpr int64_t kMaxBatch = 0x7fffffff;
 
 static int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -53,7 +56,8 @@ struct DevBuf {
 
 struct socp_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t own = nullptr;     // created by socp_ctx_create
+  hipStream_t stream = nullptr;  // where work goes: `own`, or the caller's (socp_ctx_set_stream)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int num_cu = 0;
   float last_ms = 0.f;
@@ -80,33 +84,59 @@ extern "C" void socp_params_default(socp_params* p) {
   p->reserved = 0;
 }
 
+static void ctx_free(socp_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->own && c->own != c->stream) (void)hipStreamSynchronize(c->own);
+  for (auto& b : c->buf) b.release();
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
 extern "C" int socp_ctx_create(int device, socp_ctx** out) {
   if (!out) return fail(SOCP_E_INVALID, "out is NULL");
+  *out = nullptr;
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(SOCP_E_INVALID, "bad device index");
   HIPCHK(hipSetDevice(device));
   socp_ctx* c = new socp_ctx();
   c->device = device;
+  // every partially created resource is released on an error path
+  auto bail = [&](hipError_t e, const char* what) {
+    ctx_free(c);
+    return fail(SOCP_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  };
   hipDeviceProp_t prop;
-  HIPCHK(hipGetDeviceProperties(&prop, device));
+  hipError_t e;
+  if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return bail(e, "hipGetDeviceProperties");
   c->num_cu = prop.multiProcessorCount;
-  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIPCHK(hipEventCreate(&c->ev0));
-  HIPCHK(hipEventCreate(&c->ev1));
+  if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess)
+    return bail(e, "hipStreamCreateWithFlags");
+  c->stream = c->own;
+  if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail(e, "hipEventCreate");
+  if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail(e, "hipEventCreate");
   *out = c;
   return 0;
 }
 
 extern "C" int socp_ctx_destroy(socp_ctx* c) {
-  if (!c) return 0;
-  (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
-  for (auto& b : c->buf) b.release();
-  (void)hipEventDestroy(c->ev0);
-  (void)hipEventDestroy(c->ev1);
-  (void)hipStreamDestroy(c->stream);
-  delete c;
+  ctx_free(c);
+  return 0;
+}
+
+extern "C" int socp_ctx_set_stream(socp_ctx* c, void* stream) {
+  if (!c) return fail(SOCP_E_INVALID, "ctx is NULL");
+  hipStream_t s = stream ? (hipStream_t)stream : c->own;
+  if (s == c->stream) return 0;
+  // work already queued on the old stream stays ordered before what follows
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipEventRecord(c->ev1, c->stream));
+  HIPCHK(hipStreamWaitEvent(s, c->ev1, 0));
+  c->stream = s;
   return 0;
 }
 
@@ -133,6 +163,8 @@ static int check_problem(const socp_dims* d, const int32_t* kind, const int32_t*
   if (!d) return fail(SOCP_E_INVALID, "dims is NULL");
   if (d->batch < 0 || d->n <= 0 || d->m < 0 || d->k <= 0 || d->ncones <= 0)
     return fail(SOCP_E_INVALID, "bad dims (need batch>=0, n>0, m>=0, k>0, ncones>0)");
+  if (d->batch > kMaxBatch)
+    return fail(SOCP_E_INVALID, "batch above 2^31-1 (problem indices are int32 on the device)");
   if (d->ncones > MAXC) return fail(SOCP_E_UNSUPPORTED, "too many cones");
   if (!kind || !offs || !dim) return fail(SOCP_E_INVALID, "cone arrays are NULL");
   int next = 0, deg = 0;

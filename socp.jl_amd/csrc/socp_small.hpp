@@ -77,8 +77,8 @@ enum : int {
   O_CC = O_CKIND + NCS,        // per-cone constants of the current scaling [NCC][NCS]
   O_PART = O_CC + 12 * NCS,    // segment partials [NVMAX][NCS][2 slots] (zero where unused)
   O_TOTC = O_PART + 4 * NCS * 2,  // per-cone results [2][NCS]
-  O_STAMPS = O_TOTC + 2 * NCS,  // diagnostic build: per-phase cycle totals of this wave [16]
-  O_KV = O_STAMPS + 16         // 16 k-vectors, Shape::KS apart
+  O_STAMPS = O_TOTC + 2 * NCS,  // diagnostic build: per-phase cycle totals of this wave [24]
+  O_KV = O_STAMPS + 24         // 16 k-vectors, Shape::KS apart
 };
 // per-cone constants (SOC cones), recomputed by every scaling:
 //   MU = mu, IMU = 1/mu, WB0 = wbar_0, I1 = 1/(1+wbar_0), W2 = |wbar_1|^2,
@@ -128,6 +128,7 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
 // deltas accumulated per problem and added to a global table by lane 0.
 #ifdef SOCP_DIAG
 #define NSTAMP 12
+#define NSUBSTAMP 6  // sub-phases of the H sweep, slots NSTAMP+1 ..
 // Totals live in LDS (lane 0 read-modify-writes them), so the stamps cost no
 // registers beyond the last timestamp; they are flushed once per wave.
 #define STAMP_DECL uint64_t st_last = 0;
@@ -135,10 +136,12 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
 #define STAMP(i) do { __builtin_amdgcn_s_waitcnt(0); const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
     if (threadIdx.x == 0) reinterpret_cast<unsigned long long*>(socp_lds + O_STAMPS)[i] += t_ - st_last; \
     st_last = t_; } while (0)
+#define STAMP_SUB(i) do { if constexpr (SUBST) STAMP(NSTAMP + 1 + (i)); } while (0)
 #else
 #define STAMP_DECL
 #define STAMP_START_S(obj) do {} while (0)
 #define STAMP(i) do {} while (0)
+#define STAMP_SUB(i) do {} while (0)
 #endif
 enum { SP_LOAD, SP_SCALING, SP_RESID, SP_U, SP_SYRK, SP_SWEEP_H, SP_SCHUR, SP_SOLVE, SP_STEP, SP_VOP,
        SP_STORE, SP_OTHER };
@@ -424,7 +427,7 @@ struct Small {
     // segment partials: entry (v, c, slot) is written only when cone c meets the
     // slot, the same for every problem of the launch; the rest stays zero
     for (int e = lane; e < O_TOTC - O_PART; e += 64) LDS(O_PART + e) = 0.0;
-    if (lane < 16) LDS(O_STAMPS + lane) = 0.0;  // all-zero bits: the u64 totals start at 0
+    if (lane < 24) LDS(O_STAMPS + lane) = 0.0;  // all-zero bits: the u64 totals start at 0
     SYNC();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1051,154 +1054,200 @@ struct Small {
     }
   }
 
-  // Pivot data of step C, from the (exactly symmetric) diagonal tile D: column
-  // c by DPP row_newbcast, the pivot by readlane, row c (= column c) by a row
-  // broadcast -- registers only.
-  struct Piv {
-    double cR[4];  // lane (g, cl): D[g + 4r][c]
-    double d, rinv, rowD;
-  };
-  template <int C>
-  __device__ __forceinline__ static void pivot_data(const d4& D, Piv& v) {
-    constexpr int pr = C / 4, pg = C % 4;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v.cR[r] = dpp_all<0x150 + C>(D[r]);
-    v.d = readlane_d(D[pr], 16 * pg + C);
-    v.rinv = recip(v.d);
-    v.rowD = row_bcast<pg>(D[pr]);
+  // ------------------------------------------------- H^-1 by a block sweep
+  // The inverse Li = H^-1 of densesolver.jl:47-48 (cholesky! + potrs(I)) is
+  // formed by a symmetric Gauss-Jordan sweep with 16x16 pivot tiles P; after
+  // every tile is swept the lower tiles hold -H^-1.  Per tile:
+  //   D = M_PP = L L' (its current Schur complement), W = L^-1 (VALU, below);
+  //   Y_i = W M_Pi                      (i != P, MFMA)
+  //   M_ij -= Y_i' Y_j                  (i, j != P: the Schur update in Gram
+  //                                      form, as accurate as a Cholesky step)
+  //   M_Pi <- W' Y_i = D^-1 M_Pi, M_PP <- -W'W = -D^-1          (MFMA)
+  // Every pivot of D is a Cholesky pivot of H (a Schur complement), so a
+  // pivot <= 0 or NaN fails exactly where LAPACK potrf fails inside
+  // cholesky!.  C/D-tile algebra: lane (g, cl) holds X[g+4r][cl] in register
+  // r, so register s of a tile is the k-step-s operand of mfma_f64_16x16x4,
+  // and sum_s mfma(U[s], V[s]) = U'V for any two tiles U, V.
+
+  // x^-1/2: v_rsq_f64 + two Newton steps (within 1 ulp)
+  __device__ __forceinline__ static double rsqrt_nr(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    double e = fma(-(h * y), y, 0.5);
+    y = fma(y, e, y);
+    e = fma(-(h * y), y, 0.5);
+    return fma(y, e, y);
   }
 
-  // Single-pivot steps C.. of panel P (pivot c = 16 P + C, row c of the tile is
-  // register pr of the lanes of row pg).  The pivot data of step C arrive in
-  // pv (computed by the previous step right after its tile update, so the DPP /
-  // readlane / reciprocal chain overlaps the slab work).  The lanes of row pg
-  // publish row c of every slab tile through LDS.  The diagonal tile is kept
-  // exactly symmetric: the rank-1 term is (D_ic D_cj) / d with one product for
-  // (i,j) and (j,i), and the pivot row and column are the same values times
-  // 1/d -- so its row c IS its column c, and the inverse stays a good
-  // right-inverse at kappa ~ 1e10.
-  template <int Q, int P, int C>
-  __device__ __forceinline__ void sweep_steps(d4& D, d4 (&Z)[Q], d4 (&W)[Q], d4& rv, Piv& pv, int cnt,
-                                              int& step, bool& ok) {
-    if constexpr (C < 16) {
-      constexpr int pr = C / 4, pg = C % 4;
-      if (C >= cnt) return;
+  // sum_s mfma(U[s], V[s], C) with the NEG modifiers of gfx950 f64 MFMA
+  // (blgp bit 0 negates A, bit 2 negates C)
+  template <int NEG>
+  __device__ __forceinline__ static d4 mm(const d4& U, const d4& V, d4 C) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) C = __builtin_amdgcn_mfma_f64_16x16x4f64(U[s], V[s], C, 0, 0, NEG);
+    return C;
+  }
+
+#ifndef SOCP_TILE_FACTOR
+#define SOCP_TILE_FACTOR 1
+#endif
+#ifndef SOCP_TRANSPOSE_MFMA
+#define SOCP_TRANSPOSE_MFMA 0
+#endif
+#if SOCP_TILE_FACTOR == 0
+  // Pivot J of row block B of the tile factorisation: v = register B of the
+  // (updated) D tile, w = register B of the eliminated identity.  Row J of
+  // the block (lanes of row group J) is scaled by 1/sqrt(d) and becomes row
+  // 4B+J of L' (R) and of W; the rows below it in the block take the rank-1
+  // update.  Rows above it (finished) take garbage, never read again.
+  template <int B, int J>
+  __device__ __forceinline__ void tile_pivot(double& v, double& w, double& R, double& Wb, bool& ok) const {
+    if constexpr (J < 4) {
       LANE_IDS();
-      const bool lane_c = cl == C, lane_r = g == pg;
-      double rowv[Q];  // row c of slab tile i at column cl
-      if constexpr (Q > 1) {
-        const int cb = O_COL + (step & 1) * SH::CB;
-        ++step;
-        if (lane_r) {
-#pragma unroll
-          for (int i = 0; i < Q; ++i)
-            if (i != P) LDS(cb + 16 * i + cl) = Z[i][pr];
-        }
-        SYNC();
-#pragma unroll
-        for (int i = 0; i < Q; ++i)
-          if (i != P) rowv[i] = LDS(cb + 16 * i + cl);
-      }
-      const double cR0 = pv.cR[0], cR1 = pv.cR[1], cR2 = pv.cR[2], cR3 = pv.cR[3];
-      const double cR[4] = {cR0, cR1, cR2, cR3};
-      const double rinv = pv.rinv;
-      ok = ok && (pv.d > 0.0);  // a failed pivot poisons the rest; tested once at the end
+      const double d = readlane_d(v, 16 * J + 4 * B + J);
+      ok = ok && (d > 0.0);  // NaN fails too: potrf's test
+      const double rs = rsqrt_nr(d);
+      const double vj = row_bcast<J>(v) * rs;
+      const double wj = row_bcast<J>(w) * rs;
+      const double l = dpp_all<0x150 + 4 * B + J>(v) * rs;  // D[4B+g][4B+J] / sqrt(d)
+      v = fma(-l, vj, v);
+      w = fma(-l, wj, w);
+      R = (g == J) ? vj : R;
+      Wb = (g == J) ? wj : Wb;
+      tile_pivot<B, J + 1>(v, w, R, Wb, ok);
+    }
+  }
+#endif
+  // Row blocks B.. of W = L^-1 for D = L L' (right-looking, 4 rows at a time;
+  // the rank-4 trailing update of the D and identity tiles is one MFMA each).
+  // The 4x4 diagonal block is factored in wave-uniform values (its upper
+  // triangle, as potrf('U') reads it), then every lane forms the block's rows
+  // of R = L' and of W by forward substitution from the broadcast block rows.
+  template <int B>
+  __device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok) const {
+    if constexpr (B < 4) {
+      LANE_IDS();
+      double R, Wb;
+#if SOCP_TILE_FACTOR == 0
       {
-        const double rowD = pv.rowD, cC = rowD * rinv;
+        double v = Dt[B], w = It[B];
+        R = 0.0;
+        Wb = 0.0;
+        tile_pivot<B, 0>(v, w, R, Wb, ok);
+      }
+#else
+      {
+        const double v = Dt[B], w = It[B];
+        // a_ij = D[4B+i][4B+j] (i <= j): lane (i, 4B+j) of register B
+        const double a00 = readlane_d(v, 4 * B), a01 = readlane_d(v, 4 * B + 1),
+                     a02 = readlane_d(v, 4 * B + 2), a03 = readlane_d(v, 4 * B + 3);
+        const double a11 = readlane_d(v, 16 + 4 * B + 1), a12 = readlane_d(v, 16 + 4 * B + 2),
+                     a13 = readlane_d(v, 16 + 4 * B + 3);
+        const double a22 = readlane_d(v, 32 + 4 * B + 2), a23 = readlane_d(v, 32 + 4 * B + 3);
+        const double a33 = readlane_d(v, 48 + 4 * B + 3);
+        const double rs0 = rsqrt_nr(a00);
+        const double r01 = a01 * rs0, r02 = a02 * rs0, r03 = a03 * rs0;
+        const double s11 = fma(-r01, r01, a11);
+        const double rs1 = rsqrt_nr(s11);
+        const double r12 = fma(-r01, r02, a12) * rs1, r13 = fma(-r01, r03, a13) * rs1;
+        const double s22 = fma(-r12, r12, fma(-r02, r02, a22));
+        const double rs2 = rsqrt_nr(s22);
+        const double r23 = fma(-r12, r13, fma(-r02, r03, a23)) * rs2;
+        const double s33 = fma(-r23, r23, fma(-r13, r13, fma(-r03, r03, a33)));
+        const double rs3 = rsqrt_nr(s33);
+        ok = ok && (a00 > 0.0) && (s11 > 0.0) && (s22 > 0.0) && (s33 > 0.0);  // NaN fails too
+        double V[4], X[4];
+        row_bcast4(v, V);
+        row_bcast4(w, X);
+        const double R0 = V[0] * rs0;
+        const double R1 = fma(-r01, R0, V[1]) * rs1;
+        const double R2 = fma(-r12, R1, fma(-r02, R0, V[2])) * rs2;
+        const double R3 = fma(-r23, R2, fma(-r13, R1, fma(-r03, R0, V[3]))) * rs3;
+        const double W0 = X[0] * rs0;
+        const double W1 = fma(-r01, W0, X[1]) * rs1;
+        const double W2 = fma(-r12, W1, fma(-r02, W0, X[2])) * rs2;
+        const double W3 = fma(-r23, W2, fma(-r13, W1, fma(-r03, W0, X[3]))) * rs3;
+        R = g == 0 ? R0 : (g == 1 ? R1 : (g == 2 ? R2 : R3));
+        Wb = g == 0 ? W0 : (g == 1 ? W1 : (g == 2 ? W2 : W3));
+      }
+#endif
+      W[B] = Wb;
+      if constexpr (B < 3) {
+        const d4 t = __builtin_amdgcn_mfma_f64_16x16x4f64(R, R, Dt, 0, 0, 1);   // Dt -= R'R
+        const d4 u = __builtin_amdgcn_mfma_f64_16x16x4f64(R, Wb, It, 0, 0, 1);  // It -= R'W
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const double gen = fma(-(cR[r] * rowD), rinv, D[r]);
-          const double scol = cR[r] * rinv;
-          const bool iR = (r == pr) && lane_r;
-          D[r] = (iR && lane_c) ? -rinv : (lane_c ? scol : (iR ? cC : gen));
+        for (int r = B + 1; r < 4; ++r) {
+          Dt[r] = t[r];
+          It[r] = u[r];
         }
       }
-      if constexpr (C + 1 < 16) pivot_data<C + 1>(D, pv);
-      rv[pr] = lane_r ? rinv : rv[pr];
+      tile_block<B + 1>(Dt, It, W, ok);
+    }
+  }
+  __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok) const {
+    LANE_IDS();
+    d4 It;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) It[r] = (g + 4 * r == cl) ? 1.0 : 0.0;
+    W = It;
+    tile_block<0>(Dt, It, W, ok);
+  }
+
+  // tile transpose: by MFMA against the identity (X' I), no LDS hand-off, or
+  // through LDS
+  __device__ __forceinline__ d4 ttrans(const d4& X, const d4& Id) {
+#if SOCP_TRANSPOSE_MFMA
+    return mm<0>(X, Id, (d4){0.0, 0.0, 0.0, 0.0});
+#else
+    return transpose(X);
+#endif
+  }
+
+  template <int Q, bool SUBST, int P = 0>
+  __device__ __forceinline__ void sweep_tiles(d4 (&M)[Q * (Q + 1) / 2], const d4& Id, bool& ok) {
+    if constexpr (P < Q) {
+      d4 X[Q];  // M_Pi in C/D layout (stored transposed below the pivot tile)
+#pragma unroll
+      for (int i = P + 1; i < Q; ++i) X[i] = ttrans(M[tri(i, P)], Id);
+      STAMP_SUB(0);
+      d4 W;
+      factor_tile(M[tri(P, P)], W, ok);
+      STAMP_SUB(1);
+      const d4 WT = ttrans(W, Id);
+      const d4 z = (d4){0.0, 0.0, 0.0, 0.0};
+      d4 Y[Q];
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+        if (i != P) Y[i] = mm<0>(WT, i < P ? M[tri(P, i)] : X[i], z);  // W M_Pi
+      STAMP_SUB(2);
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j)
+          if (i != P && j != P) M[tri(i, j)] = mm<1>(Y[i], Y[j], M[tri(i, j)]);  // -= Y_i'Y_j
+      STAMP_SUB(3);
 #pragma unroll
       for (int i = 0; i < Q; ++i) {
-        if (i == P) continue;
-        const double rc = rowv[i];  // M[c][col]
-        const double rs = rc * rinv;
-        W[i][pr] = lane_r ? rc : W[i][pr];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const double gen = fma(-cR[r], rs, Z[i][r]);
-          Z[i][r] = (r == pr && lane_r) ? rs : gen;
-        }
+        if (i < P) M[tri(P, i)] = mm<0>(W, Y[i], z);  // W'Y_i = D^-1 M_Pi
+        if (i > P) M[tri(i, P)] = mm<0>(Y[i], W, z);  // its transpose
       }
-      if constexpr (C % 4 == 3) SCHED_FENCE();  // bound how far the next steps' work is hoisted
-      sweep_steps<Q, P, C + 1>(D, Z, W, rv, pv, cnt, step, ok);
+      M[tri(P, P)] = mm<1>(W, W, z);  // -W'W = -D^-1
+      STAMP_SUB(4);
+      sweep_tiles<Q, SUBST, P + 1>(M, Id, ok);
     }
   }
 
-  // Symmetric Gauss-Jordan sweep of the first nact pivots of a symmetric
-  // matrix held as lower tiles in C/D layout; leaves -M^-1 there.  Pivot p is
-  // the Schur complement = (Cholesky diagonal)^2, so the failure test is the
-  // one LAPACK potrf applies inside cholesky! (ajj <= 0 or NaN).
-  //
-  // Blocked by 16-pivot panels P.  The 16 single-pivot steps run only on the
-  // panel slab [M_PP | Z] (Z_i = M_Pi, rows P, cols i != P), which they turn
-  // into [-M_PP^-1 | M_PP^-1 Z].  The rank-1 updates the single-pivot sweep
-  // would apply to every other tile are deferred: at step c the current row c
-  // of Z (rc) and 1/d_c are kept, and M_OO -= sum_c rc_c rc_c'/d_c is applied
-  // once per panel with MFMA -- the same sum of rank-1 terms (Gram form, as
-  // accurate as the unblocked sweep; the explicit -M_PP^-1-based update is not).
-  template <int Q, int P = 0>
-  __device__ __forceinline__ bool sweep(d4 (&M)[Q * (Q + 1) / 2], int nact) {
-    if constexpr (P < Q) {
-      if (16 * P >= nact) return true;
-      const int cnt = (nact - 16 * P) < 16 ? (nact - 16 * P) : 16;
-      d4 Z[Q], W[Q];
+  // Symmetric sweep of every pivot of M (lower tiles; padding rows carry an
+  // identity diagonal, so sweeping them is harmless): leaves -M^-1.
+  template <int Q, bool SUBST>
+  __device__ __forceinline__ bool sweep(d4 (&M)[Q * (Q + 1) / 2]) {
+    LANE_IDS();
+    d4 Id;
 #pragma unroll
-      for (int i = 0; i < Q; ++i) {
-        W[i] = (d4){0.0, 0.0, 0.0, 0.0};
-        if (i < P) Z[i] = M[tri(P, i)];
-        if (i > P) Z[i] = transpose(M[tri(i, P)]);
-      }
-      d4 rv = (d4){0.0, 0.0, 0.0, 0.0};  // per lane: 1/d of pivot 4s + g (Gram scaling)
-      {
-        // mirror the lower triangle of the pivot tile onto the upper one (the
-        // Gram updates of earlier panels are symmetric only to rounding)
-        d4& D = M[tri(P, P)];
-        const d4 Dt = transpose(D);
-        LANE_IDS();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) D[r] = (g + 4 * r >= cl) ? D[r] : Dt[r];
-      }
-      int step = 0;
-      bool ok = true;
-      Piv pv;
-      pivot_data<0>(M[tri(P, P)], pv);
-      sweep_steps<Q, P, 0>(M[tri(P, P)], Z, W, rv, pv, cnt, step, ok);
-      if (!ok) return false;
-      // M_OO -= sum_c rc_c rc_c' / d_c (lower tiles of every other block row /
-      // column); lane (g, cl) of k-step s holds pivot 4s + g
-#pragma unroll
-      for (int i = 0; i < Q; ++i) {
-        if (i == P) continue;
-        d4 Wn;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Wn[r] = -W[i][r] * rv[r];
-#pragma unroll
-        for (int j = i; j < Q; ++j) {
-          if (j == P) continue;
-          // tile (j, i), j >= i: += W_j' (-W_i / d)
-          d4 acc = M[tri(j, i)];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma(W[j][s], Wn[s], acc);
-          M[tri(j, i)] = acc;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < Q; ++i) {
-        if (i < P) M[tri(P, i)] = Z[i];
-        if (i > P) M[tri(i, P)] = transpose(Z[i]);
-      }
-      return sweep<Q, P + 1>(M, nact);
-    } else {
-      return true;
-    }
+    for (int r = 0; r < 4; ++r) Id[r] = (g + 4 * r == cl) ? 1.0 : 0.0;
+    bool ok = true;
+    sweep_tiles<Q, SUBST>(M, Id, ok);
+    return ok;
   }
 
   __device__ __forceinline__ d4 transpose(d4 t) {
@@ -1242,7 +1291,7 @@ struct Small {
     double* dbg = (a.dbg && a.mode == MODE_KKT) ? a.dbg + dbg_p * (int64_t)(2 * n * n + 2 * k + n * m + m * m) : nullptr;
     if (dbg) dump_sym(dbg);
 #endif
-    const bool okH = sweep<NQ>(T, n);
+    const bool okH = sweep<NQ, true>(T);
     STAMP(SP_SWEEP_H);
     if (!okH) return ST_CHOL_H;
 #pragma unroll
@@ -1320,7 +1369,7 @@ struct Small {
     }
 #endif
     SYNC();
-    const bool okS = sweep<MQ>(Sv, m);
+    const bool okS = sweep<MQ, false>(Sv);
     STAMP(SP_SCHUR);
     if (!okS) return ST_CHOL_S;
 #pragma unroll
@@ -1778,7 +1827,7 @@ struct Small {
     SYNC();
     if (lane == 0 && a.stamps) {
       const unsigned long long* st = reinterpret_cast<const unsigned long long*>(socp_lds + O_STAMPS);
-      for (int i = 0; i <= NSTAMP; ++i) atomicAdd(a.stamps + i, st[i]);
+      for (int i = 0; i <= NSTAMP + NSUBSTAMP; ++i) atomicAdd(a.stamps + i, st[i]);
     }
 #endif
   }

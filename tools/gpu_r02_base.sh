@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-2 baseline session: GPU tests, C2 bench, SQ counter passes (issue vs
+# stall split of the C2 solver kernel), phase stamps.  Each GPU step has its
+# own limit; the first failure ends the script.
+set -e
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python bench.py --no-cpu > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
+B="python bench.py --steps 1 --warmup 0 --no-cpu --batch 16384"
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_MFMA_F64 --output-format csv -d gpurun_out/sq1 -o s -- $B > gpurun_out/sq1.log 2>&1 || { tail -20 gpurun_out/sq1.log; exit 1; }
+python tools/pmc_dump.py gpurun_out/sq1
+timeout -s KILL 90 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_VALU_MUL_F64 SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/sq2 -o s -- $B > gpurun_out/sq2.log 2>&1 || { tail -20 gpurun_out/sq2.log; exit 1; }
+python tools/pmc_dump.py gpurun_out/sq2
+timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_BRANCH SQ_WAVES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 --output-format csv -d gpurun_out/sq3 -o s -- $B > gpurun_out/sq3.log 2>&1 || { tail -20 gpurun_out/sq3.log; exit 1; }
+python tools/pmc_dump.py gpurun_out/sq3
+timeout -k 10 300 python tools/stamps.py C2 > gpurun_out/stamps.log 2>&1 || { tail -30 gpurun_out/stamps.log; exit 1; }
+cat gpurun_out/stamps.log

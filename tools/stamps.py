@@ -17,7 +17,7 @@ for cname in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["C2", "C1"]):
     ctx = S.default_context()
     c, A, b, G, h = S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
     sing = torch.zeros(B, dtype=torch.uint8, device="cuda")
-    buf = torch.zeros(13, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(24, dtype=torch.int64, device="cuda")
     _lib.load().socp_debug_set_stamps(_lib.ptr(buf))
     out = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=K, tol=0.0)
     ctx.sync(); buf.zero_()
@@ -25,7 +25,11 @@ for cname in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["C2", "C1"]):
     ctx.sync()
     v = buf.cpu().numpy().astype(float)
     iters = v[12]
-    tot = v[:12].sum()
+    tot = v[:12].sum() + v[13:19].sum()
     print(f"== {cname} B={B} K={K} kernel {ctx.last_kernel_ms():.2f} ms, iters {iters:.0f}, cycles/problem-iter {tot/iters:.0f}")
     for nm, x in zip(names, v[:12]):
         print(f"   {nm:8s} {x/iters:9.0f} cyc/it  {100*x/tot:5.1f}%")
+    subs = ["sw:transp", "sw:factor", "sw:Y", "sw:gram", "sw:new", "sw:-"]
+    for nm, x in zip(subs, v[13:19]):
+        if x:
+            print(f"   {nm:9s} {x/iters:8.0f} cyc/it  {100*x/tot:5.1f}%")
