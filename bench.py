@@ -23,6 +23,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -57,32 +58,90 @@ def cone_str(cones):
     return "+".join(out)
 
 
-def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None, tol=0.0):
-    """Oracle (the reference algorithm restated in C, oracle/) on host cores."""
+def latest_traffic_json(cfg_name):
+    """Newest committed PMC traffic summary for the config (profiles/rNN_pmc_traffic[_cfg].json)."""
+    import glob
+    suffix = "" if cfg_name == "C2" else "_" + cfg_name.lower()
+    found = sorted(glob.glob(os.path.join(HERE, "profiles", f"r[0-9][0-9]_pmc_traffic{suffix}.json")))
+    return found[-1] if found else os.path.join(HERE, "profiles", f"r01_pmc_traffic{suffix}.json")
+
+
+def host_cpu_info():
+    """nproc, the CPUs this process may run on, and the lscpu model name."""
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    if model is None:
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "model": model}
+
+
+def baseline_threads():
+    """Every core this process may use -- capped by OMP_NUM_THREADS, which the
+    GPU box sets to its per-GPU CPU share (16): the machine's other cores
+    belong to other jobs."""
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None, tol=0.0, structured=False, reps=5):
+    """Oracle (the reference algorithm restated in C, oracle/) on host cores:
+    one warm-up, then the median of `reps` timed batch solves of the same
+    sample; the sample size is chosen so the reps take about budget_s."""
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle as O  # test infrastructure: timed as the baseline, never the product
-    threads = threads or min(16, os.cpu_count() or 1)
-    # one batch of a few seconds: 256 problems at C1/C2, one per thread at C4
-    chunk = 256 if flops_per_problem_iter(cfg.n, cfg.m, cfg.k) < 1e7 else threads
-    d = O.generate(cfg.cones, chunk, cfg.n, cfg.m, cfg.k, cfg.seed)
-    P = O.Params(maxit=fixed_k, tol=tol)
-    sing = [0] * chunk
-    O.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"], sing=sing,
-                  params=P, nthreads=threads)  # warm-up
-    iters, t0, reps = 0, time.perf_counter(), 0
-    while True:
+    threads = threads or baseline_threads()
+    flags = O.F_STRUCTURED if structured else 0
+    P = O.Params(maxit=fixed_k, tol=tol, flags=flags)
+    small = flops_per_problem_iter(cfg.n, cfg.m, cfg.k) < 1e7
+
+    def run(chunk, d):
+        t0 = time.perf_counter()
         r = O.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
-                          sing=sing, params=P, nthreads=threads)
-        iters += int(r["iters"].sum())
-        reps += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": iters / dt, "unit": "problem-iterations/s", "cores": threads, "kind": "port",
-            "sample": f"{reps}x{chunk} {cfg.name} problems (first {chunk} of the seeded workload), "
+                          sing=[0] * chunk, params=P, nthreads=threads)
+        return int(r["iters"].sum()), time.perf_counter() - t0
+
+    chunk = 4 * threads if small else threads
+    d = O.generate(cfg.cones, chunk, cfg.n, cfg.m, cfg.k, cfg.seed)
+    run(chunk, d)  # warm-up (page-in, thread pool)
+    _, t_probe = run(chunk, d)
+    want = budget_s / reps  # seconds per rep
+    if t_probe < want:
+        chunk = int(chunk * want / max(t_probe, 1e-4)) // threads * threads or threads
+        chunk = min(chunk, 65536)
+        d = O.generate(cfg.cones, chunk, cfg.n, cfg.m, cfg.k, cfg.seed)
+    rates, total_t = [], 0.0
+    for _ in range(reps):
+        it, dt = run(chunk, d)
+        rates.append(it / dt)
+        total_t += dt
+    rates.sort()
+    med = rates[len(rates) // 2]
+    info = host_cpu_info()
+    algo = ("oracle/socp_oracle.c structured mode (the kernels' algorithm: X = W^-1 G per cone, H = X'X, "
+            "explicit inverse; no dense iWiW)" if structured else
+            "oracle/socp_oracle.c (reference op order incl. dense iW*iW' and potrs(I) inverse)")
+    return {"value": med, "unit": "problem-iterations/s", "cores": threads, "kind": "port",
+            "per_core": med / threads, "nproc": info["nproc"], "affinity_cpus": info["affinity"],
+            "cpu_model": info["model"], "reps": [round(x, 1) for x in rates],
+            "sample": f"median of {reps} reps x {chunk} {cfg.name} problems (first {chunk} of the seeded workload), "
                       + (f"tol={tol}, maxit={fixed_k}, " if tol else f"fixed-K={fixed_k}, ")
-                      + f"oracle/socp_oracle.c (reference op order incl. dense iW*iW' and potrs(I) inverse), "
-                      f"OpenMP {threads} threads, {dt:.1f}s"}
+                      + f"{algo}, OpenMP {threads} threads (OMP_NUM_THREADS / affinity), {total_t:.1f}s timed"}
 
 
 def main():
@@ -96,10 +155,10 @@ def main():
     ap.add_argument("--mode", choices=["fixed", "reference"], default="fixed",
                     help="fixed: tol=0, K iterations (headline, SURVEY.md §8(d)(i)); reference: the "
                          "reference's stopping rule, tol=1e-5 absolute, maxit=40, per-problem masking (§8(d)(ii))")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="per CPU line (two lines)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC traffic summary (tools/pmc_traffic.py); default profiles/r01_pmc_traffic[_<config>].json")
+                    help="PMC traffic summary (tools/pmc_traffic.py); default: the newest profiles/rNN_pmc_traffic[_<config>].json")
     args = ap.parse_args()
 
     import torch
@@ -127,15 +186,18 @@ def main():
     sing = torch.zeros(B, dtype=torch.uint8, device=dev)  # uniform G (k > n) has full column rank
     ctx.sync()
     out = None
-    gathered = torch.empty((world, B, 2), dtype=torch.int32, device=dev) if world > 1 else None
+    gathered = None
+    if world > 1:
+        from socp_amd.dist import gather_outcomes
 
     def step():
-        nonlocal out
-        out = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=tol, ctx=ctx, out=out)
+        nonlocal out, gathered
+        out = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=tol, ctx=ctx, out=out,
+                            res=world > 1)
         if world > 1:
-            ctx.sync()
-            local_st = torch.stack([out["status"], out["iters"]], dim=1)
-            dist.all_gather_into_tensor(gathered.view(-1, 2), local_st)
+            # the path's only exchange: every problem's 32-byte outcome record
+            # (status, iters, ||rd||, ||rp||, z's) to every rank, on torch's stream
+            gathered = gather_outcomes(out["status"], out["iters"], out["res"])
 
     for _ in range(args.warmup):
         step()
@@ -178,8 +240,7 @@ def main():
         else:
             achieved, peak, unit = F * iters_per_launch / (kms * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
         traffic = None
-        tj_path = args.traffic_json or os.path.join(
-            HERE, "profiles", "r01_pmc_traffic.json" if cfg.name == "C2" else f"r01_pmc_traffic_{cfg.name.lower()}.json")
+        tj_path = args.traffic_json or latest_traffic_json(cfg.name)
         if os.path.exists(tj_path):
             try:
                 tj = json.load(open(tj_path))
@@ -187,6 +248,7 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        hbm_gbs = traffic / (kms * 1e-3) / 1e9 if traffic else None
         line = {
             "metric": "IPM iters/sec, 65k-batch n=64 dense SOCP at 1/2/4/8 GPU; achieved HBM GB/s",
             "value": iters_total / dt,
@@ -218,6 +280,8 @@ def main():
                 "unit": unit,
                 "frac": achieved / peak,
                 "traffic": traffic,
+                "hbm_gbs": hbm_gbs,
+                "traffic_source": os.path.relpath(tj_path, HERE) if traffic else None,
                 "flops_per_problem_iter": F,
                 "bytes_per_problem_iter": Bq,
                 "problem_iters_per_launch": iters_per_launch,
@@ -225,6 +289,8 @@ def main():
         }
         if not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol)
+            line["cpu_baseline_structured"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol,
+                                                           structured=True)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -92,12 +92,24 @@ int socp_ctx_destroy(socp_ctx* ctx);
 int socp_ctx_sync(socp_ctx* ctx);
 /* hipStream_t of the context (as void*) so callers can order their own work. */
 void* socp_ctx_stream(socp_ctx* ctx);
+/* Make the context issue its work on the caller's hipStream_t (as void*), e.g.
+ * torch.cuda.current_stream().cuda_stream, so the solve is ordered after the
+ * caller's producers of its inputs and before their consumers.  NULL is HIP's
+ * null (default) stream -- torch's default current stream.  socp_ctx_reset_stream
+ * returns to the context's own stream.  Work already queued on the previous
+ * stream stays ordered before later work (an event wait is inserted). */
+int socp_ctx_set_stream(socp_ctx* ctx, void* stream);
+int socp_ctx_reset_stream(socp_ctx* ctx);
 
-/* 1 if a compiled kernel accepts the dims: the register-resident kernel
- * (n, m <= 64, k <= 128, <= 8 cones; one wavefront per problem) or the blocked
- * kernel (n, m <= 512, <= 64 cones, the problem's vectors within the 160 KiB LDS
- * of a CU -- C4, n=512 m=64 k=640, uses 126 KiB; one 512-thread workgroup per
- * problem).  Other shapes return SOCP_E_UNSUPPORTED from the solve entries. */
+/* 1 if a compiled kernel accepts the dims: the register-resident kernel (one
+ * wavefront per problem, <= 8 cones, m <= 64; k <= 128 for n <= 48, k <= 96
+ * for 48 < n <= 64: the compiled variant table, socp.jl_amd/csrc/gen_inst.py)
+ * or the blocked kernel (n, m <= 512, <= 64 cones, the problem's vectors within
+ * the 160 KiB LDS of a CU -- C4, n=512 m=64 k=640, uses 126 KiB; one
+ * 512-thread workgroup per problem), which also takes every register-kernel
+ * shape it can hold.  Other shapes return SOCP_E_UNSUPPORTED from the solve
+ * entries.  Every entry rejects batch > 2^31-1 (device problem indices are
+ * int32). */
 int socp_supported(const socp_dims* dims);
 
 /* Batched solve: replaces solve_socp(prob, SolverState(prob, DenseSolver(prob)))
@@ -112,7 +124,11 @@ int socp_supported(const socp_dims* dims);
  *                        (the reference returns State(x,y,z,s), solver.jl:152).
  *   iters, status      : out, per problem (int32); iters = completed Newton steps.
  * With SOCP_F_DEVICE_PTRS the call is stream-ordered and returns without
- * synchronising; otherwise it copies, solves and synchronises. */
+ * synchronising; otherwise it copies, solves and synchronises.
+ * Diagnostics: with SOCP_DUMP_DIR=<dir> in the environment, the first
+ * SOCP_DUMP_COUNT (default 1) problems of every batch are written to
+ * <dir>/problem<p>_{A,G,c,b,h,initv,cones}.txt, as the reference's commented
+ * dumps do (solver.jl:48-67,75-82). */
 int socp_batch_solve(socp_ctx* ctx, const socp_dims* dims,
                      const int32_t* cone_kind, const int32_t* cone_offs, const int32_t* cone_dim,
                      const double* c, const double* A, const double* b,
@@ -193,6 +209,20 @@ int socp_comm_init(socp_ctx* ctx, int nranks, int rank, const unsigned char* id,
 int socp_comm_destroy(socp_comm* comm);
 int socp_allgather_status(socp_comm* comm, int64_t batch, const int32_t* status, const int32_t* iters,
                           int32_t* out);
+/* The SURVEY.md §8(e) record: per problem 32 bytes -- status, iters and the
+ * exit-test quantities ||rd||, ||rp||, z's at the returned iterate
+ * (solver.jl:109-122; res[] of socp_batch_solve_ex, NaN where res is NULL).
+ * out[r*B + p] is rank r's problem p; device pointers; stream-ordered.  A comm
+ * must be destroyed before the context it was created on. */
+typedef struct socp_outcome {
+  int32_t status;
+  int32_t iters;
+  double res_dual;   /* ||A'y + G'z + c|| */
+  double res_primal; /* ||Ax - b||        */
+  double gap;        /* z's               */
+} socp_outcome;
+int socp_allgather_outcomes(socp_comm* comm, int64_t batch, const int32_t* status, const int32_t* iters,
+                            const double* res, socp_outcome* out);
 
 /* Timing of the last solve's main kernel, measured with HIP events on the
  * context's stream (milliseconds), and its name. */

@@ -46,6 +46,7 @@ class Params(C.Structure):
 
 
 F_WARM_START = 2
+F_STRUCTURED = 16  # oracle-only: the build's structured algorithm (CPU baseline line)
 
 
 def build(force: bool = False) -> str:

@@ -221,8 +221,14 @@ typedef struct {
 #define M(A, ld, i, j) (A)[(size_t)(j) * (ld) + (i)]
 
 /* compute_scaling (scalings.jl:22-110) */
+static void compute_scaling_x(const cones_t* C, scaling_t* S, const double* s, const double* z,
+                              int* dom, int structured);
 static void compute_scaling(const cones_t* C, scaling_t* S, const double* s, const double* z,
                             int* dom) {
+  compute_scaling_x(C, S, s, z, dom, 0);
+}
+static void compute_scaling_x(const cones_t* C, scaling_t* S, const double* s, const double* z,
+                              int* dom, int structured) {
   int k = S->k;
   for (int c = 0; c < C->ncones; ++c) {
     int o = C->offs[c], dim = C->dim[c];
@@ -264,18 +270,21 @@ static void compute_scaling(const cones_t* C, scaling_t* S, const double* s, con
     double denom = wb[0] + 1.0;
     double mu = jsqrt(nrms / nrmz, dom);
     S->mu[c] = mu;
+    if (!structured)
     for (int j = 1; j <= bl; ++j)
       for (int i = 1; i <= bl; ++i) {
         double cellv = ((i == j) ? 1.0 : 0.0) + wb[i] * wb[j] / denom;
         M(S->W, k, o + i, o + j) = cellv * mu;
         M(S->iW, k, o + i, o + j) = cellv / mu;
       }
-    for (int i = 0; i < dim; ++i) M(S->W, k, o, o + i) = wb[i] * mu;
-    M(S->iW, k, o, o) = wb[0] / mu;
-    for (int i = 1; i < dim; ++i) {
-      M(S->W, k, o + i, o) = wb[i] * mu;
-      M(S->iW, k, o, o + i) = -wb[i] / mu;
-      M(S->iW, k, o + i, o) = -wb[i] / mu;
+    if (!structured) {
+      for (int i = 0; i < dim; ++i) M(S->W, k, o, o + i) = wb[i] * mu;
+      M(S->iW, k, o, o) = wb[0] / mu;
+      for (int i = 1; i < dim; ++i) {
+        M(S->W, k, o + i, o) = wb[i] * mu;
+        M(S->iW, k, o, o + i) = -wb[i] / mu;
+        M(S->iW, k, o + i, o) = -wb[i] / mu;
+      }
     }
     double ziv = zik[0], siv = sik[0];
     double tmv1 = jsqrt(nrms * nrmz, dom);
@@ -286,7 +295,9 @@ static void compute_scaling(const cones_t* C, scaling_t* S, const double* s, con
     for (int i = 1; i < dim; ++i) S->l[o + i] = (sik[i] + zik[i]) * mult;
     S->l[o] = gamma * tmv1;
   }
-  /* iWiW = iW * iW' (scalings.jl:108): dense k^3 GEMM as the reference does */
+  /* iWiW = iW * iW' (scalings.jl:108): dense k^3 GEMM as the reference does
+     (the structured mode applies W^-1 per cone instead and never forms it) */
+  if (structured) return;
   for (int j = 0; j < k; ++j)
     for (int i = 0; i < k; ++i) {
       double acc = 0.0;
@@ -370,14 +381,32 @@ static void potrs_u(const double* U, int n, double* b) {
 
 typedef struct {
   int n, m, k, sing;
+  int structured;        /* OR_F_STRUCTURED: the build's algorithm, not the reference op order */
+  const cones_t* C;
   const double *A, *G; /* column-major m x n, k x n */
   double *AA, *GWiWi, *H, *Li, *ALi, *S;
   double *k0, *k1, *k2, *m0, *n0, *n1;
 } dense_t;
 
 /* setup_iter(::DenseSolver) (densesolver.jl:41-52, with the fixes); returns 0/2/3 */
+static void iscale_w(const cones_t* C, const scaling_t* S, const double* x, double* op);
 static int setup_iter(dense_t* D, const scaling_t* S) {
   int n = D->n, m = D->m, k = D->k;
+  if (D->structured) {
+    /* X = W^-1 G column by column (iscale!, O(k) per column), H = X'X (one
+       triangle, mirrored): the reference's iWiW GEMM, G'*iWiW and *G done
+       structurally -- the algorithm the MI355X kernels run.  X is kept in the
+       GWiWi buffer (k x n, column-major). */
+    double* X = D->GWiWi;
+    for (int a = 0; a < n; ++a) iscale_w(D->C, S, D->G + (size_t)a * k, X + (size_t)a * k);
+    for (int b = 0; b < n; ++b)
+      for (int a = 0; a <= b; ++a) {
+        double acc = 0.0;
+        for (int i = 0; i < k; ++i) acc += X[(size_t)a * k + i] * X[(size_t)b * k + i];
+        M(D->H, n, a, b) = acc;
+        M(D->H, n, b, a) = acc;
+      }
+  } else {
   for (int j = 0; j < k; ++j)
     for (int a = 0; a < n; ++a) {
       double acc = 0.0;
@@ -390,6 +419,7 @@ static int setup_iter(dense_t* D, const scaling_t* S) {
       for (int i = 0; i < k; ++i) acc += M(D->GWiWi, n, a, i) * M(D->G, k, i, b);
       M(D->H, n, a, b) = acc;
     }
+  }
   if (D->sing)
     for (size_t q = 0; q < (size_t)n * n; ++q) D->H[q] += D->AA[q];
   if (potrf_u(D->H, n)) return 2;
@@ -424,6 +454,15 @@ static void solve_kkt(dense_t* D, const cones_t* C, const scaling_t* S, const do
   iprod(C, D->k0, S->l, ds);
   scale_w(C, S, D->k0, D->k1);
   for (int i = 0; i < k; ++i) D->k2[i] = dz[i] - D->k1[i];
+  if (D->structured) {
+    /* G'W^-1W^-1 k2 = X'(W^-1 k2) */
+    iscale_w(C, S, D->k2, cz);
+    for (int a = 0; a < n; ++a) {
+      double acc = 0.0;
+      for (int i = 0; i < k; ++i) acc += D->GWiWi[(size_t)a * k + i] * cz[i];
+      D->n0[a] = acc;
+    }
+  } else
   for (int a = 0; a < n; ++a) {
     double acc = 0.0;
     for (int i = 0; i < k; ++i) acc += M(D->GWiWi, n, a, i) * D->k2[i];
@@ -465,6 +504,11 @@ static void solve_kkt(dense_t* D, const cones_t* C, const scaling_t* S, const do
     D->k1[i] = acc;
   }
   for (int i = 0; i < k; ++i) D->k1[i] -= D->k2[i];
+  if (D->structured) {
+    /* iWiW k1 = W^-1 (W^-1 k1); cs (written last) is the scratch */
+    iscale_w(C, S, D->k1, cs);
+    iscale_w(C, S, cs, cz);
+  } else
   for (int i = 0; i < k; ++i) {
     double acc = 0.0;
     for (int q = 0; q < k; ++q) acc += M(S->iWiW, k, i, q) * D->k1[q];
@@ -531,6 +575,8 @@ static int ws_init(ws_t* w, int n, int m, int k, int ncones, int maxdim) {
   w->D.n = n;
   w->D.m = m;
   w->D.k = k;
+  w->D.structured = 0;
+  w->D.C = NULL;
   w->D.AA = carve(&p, sizeof(double) * n * n);
   w->D.H = carve(&p, sizeof(double) * n * n);
   w->D.Li = carve(&p, sizeof(double) * n * n);
@@ -610,6 +656,7 @@ typedef struct {
 } params_t; /* mirrors socp_params */
 
 #define F_WARM 2
+#define OR_F_STRUCTURED 16 /* oracle-only: the build's structured algorithm (CPU baseline) */
 
 static double dot(const double* a, const double* b, int n) {
   double s = 0.0;
@@ -671,6 +718,8 @@ static void solve_one(ws_t* w, const cones_t* C, const double* c, const double* 
   D->A = A;
   D->G = G;
   D->sing = sing;
+  D->C = C;
+  D->structured = (P->flags & OR_F_STRUCTURED) != 0;
   /* DenseSolver ctor: AA = A'A (densesolver.jl:31-32) */
   for (int bq = 0; bq < n; ++bq)
     for (int a = 0; a < n; ++a) {
@@ -699,7 +748,7 @@ static void solve_one(ws_t* w, const cones_t* C, const double* c, const double* 
       memcpy(t + n + m + k, s, sizeof(double) * k);
     }
     int dom = 0;
-    compute_scaling(C, S, s, z, &dom);
+    compute_scaling_x(C, S, s, z, &dom, D->structured);
     if (dom) {
       status = 4;
       break;
@@ -879,6 +928,7 @@ EXPORT int or_kkt_single(int nc, const int32_t* kind, const int32_t* offs, const
   w.D.A = A;
   w.D.G = G;
   w.D.sing = sing;
+  w.D.C = &C;
   for (int bq = 0; bq < n; ++bq)
     for (int a = 0; a < n; ++a) {
       double acc = 0.0;

@@ -128,9 +128,7 @@ extern "C" int socp_ctx_destroy(socp_ctx* c) {
   return 0;
 }
 
-extern "C" int socp_ctx_set_stream(socp_ctx* c, void* stream) {
-  if (!c) return fail(SOCP_E_INVALID, "ctx is NULL");
-  hipStream_t s = stream ? (hipStream_t)stream : c->own;
+static int ctx_switch_stream(socp_ctx* c, hipStream_t s) {
   if (s == c->stream) return 0;
   // work already queued on the old stream stays ordered before what follows
   HIPCHK(hipSetDevice(c->device));
@@ -138,6 +136,18 @@ extern "C" int socp_ctx_set_stream(socp_ctx* c, void* stream) {
   HIPCHK(hipStreamWaitEvent(s, c->ev1, 0));
   c->stream = s;
   return 0;
+}
+
+// `stream` is taken literally: NULL is HIP's null (default) stream, which is
+// torch's default current stream.
+extern "C" int socp_ctx_set_stream(socp_ctx* c, void* stream) {
+  if (!c) return fail(SOCP_E_INVALID, "ctx is NULL");
+  return ctx_switch_stream(c, (hipStream_t)stream);
+}
+
+extern "C" int socp_ctx_reset_stream(socp_ctx* c) {
+  if (!c) return fail(SOCP_E_INVALID, "ctx is NULL");
+  return ctx_switch_stream(c, c->own);
 }
 
 extern "C" int socp_ctx_sync(socp_ctx* c) {
@@ -326,6 +336,64 @@ static int copy_back(socp_ctx* ctx, T* user, const T* devp, size_t count, bool d
     if (rc_) return rc_; \
   } while (0)
 
+// ------------------------------------------------------- problem dumps
+// SOCP_DUMP_DIR=<dir> (env): every batch solve writes the first
+// SOCP_DUMP_COUNT (default 1) problems of the batch as text, one file per
+// quantity, as the reference's commented-out dumps do (solver.jl:48-67: A, G,
+// c, b, h, cones; :75-82: the init right-hand side initv = [-c; b; h]).
+// Matrices are written one row per line.  Diagnostic only: it synchronises.
+static void dump_mat(const char* dir, int64_t p, const char* name, const double* v, int rows, int cols) {
+  char fn[1024];
+  snprintf(fn, sizeof(fn), "%s/problem%lld_%s.txt", dir, (long long)p, name);
+  FILE* f = fopen(fn, "w");
+  if (!f) return;
+  for (int i = 0; i < rows; ++i) {
+    for (int j = 0; j < cols; ++j) fprintf(f, j ? " %.17g" : "%.17g", v[(size_t)j * rows + i]);
+    fputc('\n', f);
+  }
+  fclose(f);
+}
+static int dump_problems(socp_ctx* ctx, const SmallArgs& a) {
+  const char* dir = getenv("SOCP_DUMP_DIR");
+  if (!dir || !*dir) return 0;
+  const char* cnt = getenv("SOCP_DUMP_COUNT");
+  int64_t np = cnt ? atoll(cnt) : 1;
+  if (np > a.B) np = a.B;
+  const int n = a.n, m = a.m, k = a.k;
+  std::vector<double> buf((size_t)k * n + (size_t)m * n + n + m + k + n + m + k);
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  for (int64_t p = 0; p < np; ++p) {
+    double* G = buf.data();
+    double* A = G + (size_t)k * n;
+    double* c = A + (size_t)m * n;
+    double* b = c + n;
+    double* h = b + m;
+    double* iv = h + k;
+    HIPCHK(hipMemcpy(G, a.G + p * (int64_t)k * n, sizeof(double) * k * n, hipMemcpyDefault));
+    if (m) HIPCHK(hipMemcpy(A, a.A + p * (int64_t)m * n, sizeof(double) * m * n, hipMemcpyDefault));
+    HIPCHK(hipMemcpy(c, a.c + p * n, sizeof(double) * n, hipMemcpyDefault));
+    if (m) HIPCHK(hipMemcpy(b, a.b + p * m, sizeof(double) * m, hipMemcpyDefault));
+    HIPCHK(hipMemcpy(h, a.h + p * k, sizeof(double) * k, hipMemcpyDefault));
+    for (int j = 0; j < n; ++j) iv[j] = -c[j];
+    for (int i = 0; i < m; ++i) iv[n + i] = b[i];
+    for (int i = 0; i < k; ++i) iv[n + m + i] = h[i];
+    dump_mat(dir, p, "A", A, m, n);
+    dump_mat(dir, p, "G", G, k, n);
+    dump_mat(dir, p, "c", c, n, 1);
+    dump_mat(dir, p, "b", b, m, 1);
+    dump_mat(dir, p, "h", h, k, 1);
+    dump_mat(dir, p, "initv", iv, n + m + k, 1);
+    char fn[1024];
+    snprintf(fn, sizeof(fn), "%s/problem%lld_cones.txt", dir, (long long)p);
+    if (FILE* f = fopen(fn, "w")) {
+      for (int q = 0; q < a.nc; ++q)
+        fprintf(f, "%s(%d,%d)\n", a.cones.kind[q] == POC_K ? "POC" : "SOC", a.cones.offs[q], a.cones.dim[q]);
+      fclose(f);
+    }
+  }
+  return 0;
+}
+
 extern "C" int socp_batch_solve_ex(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,
                                    const int32_t* cone_offs, const int32_t* cone_dim,
                                    const double* c, const double* A, const double* b,
@@ -382,6 +450,7 @@ extern "C" int socp_batch_solve_ex(socp_ctx* ctx, const socp_dims* dims, const i
   TRY(stage_out(ctx, X::B_RES, res, (size_t)B * 3, dev, false, &a.res));
   if (ctx->buf[X::B_CNT].ensure(256)) return fail(SOCP_E_NOMEM, "device allocation failed");
   a.counter = (int32_t*)ctx->buf[X::B_CNT].p;
+  TRY(dump_problems(ctx, a));
   TRY(v ? launch_small(ctx, a, v) : launch_large(ctx, a));
   TRY(copy_back(ctx, x, a.x, (size_t)B * n, dev));
   TRY(copy_back(ctx, y, a.y, (size_t)B * m, dev));
@@ -608,6 +677,7 @@ extern "C" int socp_generate(socp_ctx* ctx, const socp_dims* dims, const int32_t
   int degree = 0;
   TRY(check_problem(dims, cone_kind, cone_offs, cone_dim, &a.cones, &degree));
   if (dims->batch == 0) return 0;
+  if (first_problem < 0) return fail(SOCP_E_INVALID, "negative first_problem");
   if (!c || !G || !h || (dims->m > 0 && (!A || !b))) return fail(SOCP_E_INVALID, "NULL data pointer");
   if ((uint64_t)dims->k * dims->n + (uint64_t)dims->m * dims->n + dims->n + dims->m + 2 * dims->k >= (1ull << 24))
     return fail(SOCP_E_UNSUPPORTED, "problem too large for the 24-bit element counter");
@@ -636,43 +706,55 @@ extern "C" int socp_generate(socp_ctx* ctx, const socp_dims* dims, const int32_t
 // socp_pack_csc: one workgroup per problem; the problem's dense block is
 // zeroed by the workgroup, then every thread scatters a strided share of the
 // nonzeros (column by column: the column of nonzero e is found by a binary
-// search of colptr, so the scatter is one pass over nz).  Duplicates are
-// summed with atomics only where they occur: a nonzero whose predecessor in
-// the same column has the same row index adds instead of storing.
+// search of colptr, so the scatter is one pass over nz).  A first pass checks
+// that every column's row indices are strictly increasing; a problem where one
+// is not (duplicates, or unsorted indices as a hand-built CSC may have) sums
+// every entry with atomics instead of storing it, so repeated (i, j) entries
+// add up, as sparse() does.  Sums of three or more duplicates may then round
+// in either order.
 namespace {
+__device__ __forceinline__ int csc_col(const int64_t* cp, int cols, int64_t base, int64_t e) {
+  int lo = 0, hi = cols;  // invariant: cp[lo] - base <= e < cp[hi] - base
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (cp[mid] - base <= e) lo = mid; else hi = mid;
+  }
+  return lo;
+}
 __global__ void __launch_bounds__(256) socp_pack_csc_kernel(int32_t rows, int32_t cols, const int64_t* nz_offs,
                                                            const int64_t* colptr, const int64_t* rowval,
                                                            const double* nzval, int64_t base, double* dense,
                                                            int32_t* err) {
+  __shared__ int unsorted;
   const int64_t p = blockIdx.x;
   const int64_t rc = (int64_t)rows * cols;
   double* D = dense + p * rc;
+  if (threadIdx.x == 0) unsorted = 0;
   for (int64_t e = threadIdx.x; e < rc; e += blockDim.x) D[e] = 0.0;
-  __syncthreads();
   const int64_t* cp = colptr + p * (int64_t)(cols + 1);
   const int64_t n0 = nz_offs[p], nnz = nz_offs[p + 1] - n0;
+  __syncthreads();
   if (cp[0] - base != 0 || cp[cols] - base != nnz) {
     if (threadIdx.x == 0) atomicOr(err, 1);
     return;
   }
+  for (int64_t e = threadIdx.x; e + 1 < nnz; e += blockDim.x) {
+    const int j = csc_col(cp, cols, base, e);
+    if (e + 1 < cp[j + 1] - base && rowval[n0 + e + 1] <= rowval[n0 + e]) unsorted = 1;
+  }
+  __syncthreads();
+  const bool add = unsorted != 0;
   for (int64_t e = threadIdx.x; e < nnz; e += blockDim.x) {
-    // column j: the last j with cp[j] - base <= e
-    int lo = 0, hi = cols;  // invariant: cp[lo] - base <= e < cp[hi] - base
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (cp[mid] - base <= e) lo = mid; else hi = mid;
-    }
+    const int j = csc_col(cp, cols, base, e);
     const int64_t i = rowval[n0 + e] - base;
     if (i < 0 || i >= rows) {
       atomicOr(err, 2);
       continue;
     }
-    const bool dup = e > cp[lo] - base && rowval[n0 + e - 1] - base == i;
-    const bool has_dup_after = e + 1 < cp[lo + 1] - base && rowval[n0 + e + 1] - base == i;
-    if (dup || has_dup_after)
-      atomicAdd(D + (int64_t)lo * rows + i, nzval[n0 + e]);
+    if (add)
+      atomicAdd(D + (int64_t)j * rows + i, nzval[n0 + e]);
     else
-      D[(int64_t)lo * rows + i] = nzval[n0 + e];
+      D[(int64_t)j * rows + i] = nzval[n0 + e];
   }
 }
 }  // namespace
@@ -683,6 +765,7 @@ extern "C" int socp_pack_csc(socp_ctx* ctx, int64_t batch, int32_t rows, int32_t
   if (!ctx) return fail(SOCP_E_INVALID, "ctx is NULL");
   if (batch < 0 || rows < 0 || cols < 0 || (index_base != 0 && index_base != 1))
     return fail(SOCP_E_INVALID, "bad batch/rows/cols/index_base");
+  if (batch > kMaxBatch) return fail(SOCP_E_INVALID, "batch above 2^31-1 (one workgroup per problem)");
   if (batch == 0 || (int64_t)rows * cols == 0) return 0;
   if (!nz_offs || !colptr || !dense) return fail(SOCP_E_INVALID, "NULL pointer");
   HIPCHK(hipSetDevice(ctx->device));
@@ -729,6 +812,22 @@ const Rccl* rccl() {
   return r.ok ? &r : nullptr;
 }
 
+// 32-byte outcome record (include/socp.h socp_outcome): status, iters, and the
+// exit-test quantities ||rd||, ||rp||, z's (solver.jl:109-122)
+__global__ void socp_outcome_kernel(int64_t B, const int32_t* __restrict__ status, const int32_t* __restrict__ iters,
+                                    const double* __restrict__ res, socp_outcome* __restrict__ rec) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < B) {
+    socp_outcome o;
+    o.status = status[p];
+    o.iters = iters[p];
+    o.res_dual = res ? res[3 * p] : NAN;
+    o.res_primal = res ? res[3 * p + 1] : NAN;
+    o.gap = res ? res[3 * p + 2] : NAN;
+    rec[p] = o;
+  }
+}
+
 __global__ void socp_pair_kernel(int64_t B, const int32_t* __restrict__ status, const int32_t* __restrict__ iters,
                                  int32_t* __restrict__ pairs) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -740,7 +839,8 @@ __global__ void socp_pair_kernel(int64_t B, const int32_t* __restrict__ status, 
 }  // namespace
 
 struct socp_comm {
-  socp_ctx* ctx = nullptr;
+  socp_ctx* ctx = nullptr;  // must outlive the comm (destroy the comm first)
+  int device = 0;
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0;
   DevBuf pairs;
@@ -774,6 +874,7 @@ extern "C" int socp_comm_init(socp_ctx* ctx, int nranks, int rank, const unsigne
   memcpy(&u, id, sizeof(u));
   auto* c = new socp_comm();
   c->ctx = ctx;
+  c->device = ctx->device;
   c->nranks = nranks;
   c->rank = rank;
   const ncclResult_t r = R->init_rank(&c->comm, nranks, u, rank);
@@ -788,8 +889,8 @@ extern "C" int socp_comm_init(socp_ctx* ctx, int nranks, int rank, const unsigne
 extern "C" int socp_comm_destroy(socp_comm* comm) {
   if (!comm) return 0;
   const Rccl* R = rccl();
+  (void)hipSetDevice(comm->device);
   if (R && comm->comm) (void)R->destroy(comm->comm);
-  (void)hipSetDevice(comm->ctx->device);
   comm->pairs.release();
   delete comm;
   return 0;
@@ -810,5 +911,24 @@ extern "C" int socp_allgather_status(socp_comm* comm, int64_t batch, const int32
                      status, iters, pairs);
   HIPCHK(hipGetLastError());
   RCCLCHK(R, R->all_gather(pairs, out, (size_t)batch * 2, ncclInt32, comm->comm, ctx->stream));
+  return 0;
+}
+
+extern "C" int socp_allgather_outcomes(socp_comm* comm, int64_t batch, const int32_t* status, const int32_t* iters,
+                                       const double* res, socp_outcome* out) {
+  if (!comm) return fail(SOCP_E_INVALID, "comm is NULL");
+  if (batch < 0) return fail(SOCP_E_INVALID, "negative batch");
+  if (batch == 0) return 0;
+  if (!status || !iters || !out) return fail(SOCP_E_INVALID, "NULL pointer");
+  const Rccl* R = rccl();
+  socp_ctx* ctx = comm->ctx;
+  HIPCHK(hipSetDevice(ctx->device));
+  if (comm->pairs.ensure((size_t)batch * sizeof(socp_outcome))) return fail(SOCP_E_NOMEM, "device allocation failed");
+  socp_outcome* rec = (socp_outcome*)comm->pairs.p;
+  hipLaunchKernelGGL(socp_outcome_kernel, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, ctx->stream, batch,
+                     status, iters, res, rec);
+  HIPCHK(hipGetLastError());
+  // records travel as raw bytes: 32 B each, one ring all-gather over xGMI
+  RCCLCHK(R, R->all_gather(rec, out, (size_t)batch * sizeof(socp_outcome), ncclUint8, comm->comm, ctx->stream));
   return 0;
 }

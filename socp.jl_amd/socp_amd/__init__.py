@@ -96,6 +96,23 @@ def _host(a, dtype=np.float64):
     return np.ascontiguousarray(a, dtype=dtype)
 
 
+def _size(a):
+    return a.numel() if _is_torch(a) else np.size(a)
+
+
+def _check_sizes(B, **arrays):
+    """Every array must hold exactly its batch-stacked element count (the C ABI
+    reads that many elements from each pointer)."""
+    if B > _lib.MAX_BATCH:
+        raise ValueError(f"batch {B} above 2^31-1")
+    for name, (a, want) in arrays.items():
+        if a is None:
+            continue
+        got = _size(a)
+        if got != want:
+            raise ValueError(f"{name}: {got} elements, expected {want} (batch {B})")
+
+
 def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5, step=0.99,
                 sigma_exp=3, init_eps=1e-10, warm=None, ctx=None, res=False, out=None, force_large=False):
     """Solve a batch of independent problems (same dims and cone structure).
@@ -107,11 +124,19 @@ def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5,
     force_large runs the blocked kernel (socp_large.hip) even where the
     register-resident one applies.  Returns dict(x, y, z, s, iters, status[, res]).
     """
-    ctx = ctx or default_context()
     L = _lib.load()
     kind, offs, dim = cone_arrays(cones)
-    B = (c.numel() if _is_torch(c) else np.size(c)) // n
+    B = _size(c) // n
+    if B * n != _size(c):
+        raise ValueError(f"c: {_size(c)} elements is not a multiple of n={n}")
+    _check_sizes(B, A=(A if m else None, B * m * n), b=(b if m else None, B * m), G=(G, B * k * n),
+                 h=(h, B * k), sing=(sing, B))
+    if warm is not None:
+        wx, wy, wz, ws = warm
+        _check_sizes(B, warm_x=(wx, B * n), warm_y=(wy if m else None, B * m), warm_z=(wz, B * k),
+                     warm_s=(ws, B * k))
     dims = _lib.Dims(B, n, m, k, len(kind))
+    ctx = ctx or default_context()
     dev = _is_torch(G)
     flags = F_DEVICE_PTRS if dev else 0
     if warm is not None:
@@ -123,6 +148,7 @@ def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5,
     if dev:
         import torch
         devc = G.device
+        ctx.bind_torch_stream()  # ordered after torch's producers of the inputs
         if out is None:
             f64 = dict(dtype=torch.float64, device=devc)
             out = dict(x=torch.empty(B * n, **f64), y=torch.empty(max(B * m, 1), **f64),
@@ -164,11 +190,15 @@ def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5,
 def batch_kkt_solve(cones, n, m, k, A, G, sing, s, z, dx, dy, dz, ds, *, ctx=None, force_large=False):
     """One KKT solve per problem at iterate (s, z): scaling + setup_iter + solve_kkt
     (densesolver.jl:41-90) on the GPU.  Host (numpy) arrays.  Returns dict(cx,cy,cz,cs,status)."""
-    ctx = ctx or default_context()
     L = _lib.load()
     kind, offs, dim = cone_arrays(cones)
     B = np.size(s) // k
+    if B * k != np.size(s):
+        raise ValueError(f"s: {np.size(s)} elements is not a multiple of k={k}")
+    _check_sizes(B, A=(A if m else None, B * m * n), G=(G, B * k * n), sing=(sing, B), z=(z, B * k),
+                 dx=(dx, B * n), dy=(dy if m else None, B * m), dz=(dz, B * k), ds=(ds, B * k))
     dims = _lib.Dims(B, n, m, k, len(kind))
+    ctx = ctx or default_context()
     cx, cy, cz, cs = np.zeros(B * n), np.zeros(max(B * m, 1)), np.zeros(B * k), np.zeros(B * k)
     st = np.zeros(B, np.int32)
     p = _lib.ptr
@@ -194,6 +224,7 @@ def generate(cones, B, n, m, k, seed, first_problem=0, *, ctx=None, device=None)
     kind, offs, dim = cone_arrays(cones)
     dims = _lib.Dims(B, n, m, k, len(kind))
     p = _lib.ptr
+    ctx.bind_torch_stream()
     _lib.check(_lib.load().socp_generate(ctx.handle, dims, p(kind), p(offs), p(dim), seed,
                                          first_problem, p(c), p(A), p(b), p(G), p(h)))
     return c, A[:B * m * n], b[:B * m], G, h
@@ -213,7 +244,14 @@ def pack_csc(mats, rows=None, cols=None, *, index_base=1, ctx=None, device=None)
         nz_offs, colptr, rowval, nzval = mats
         B = nz_offs.numel() - 1
     else:
-        csc = [m.tocsc() for m in mats]
+        # canonical CSC (sorted row indices, duplicates summed in order, as
+        # Julia's sparse() stores them); the device kernel also sums unsorted
+        # or repeated entries, but only this form is bitwise reproducible
+        csc = []
+        for m in mats:
+            m = m.tocsc(copy=True)
+            m.sum_duplicates()
+            csc.append(m)
         B = len(csc)
         rows, cols = csc[0].shape if B else (rows or 0, cols or 0)
         for m in csc:
@@ -230,6 +268,7 @@ def pack_csc(mats, rows=None, cols=None, *, index_base=1, ctx=None, device=None)
                              if B and nz[-1] else np.zeros(1), dtype=torch.float64, device=dev)
     out = torch.empty(max(B * rows * cols, 1), dtype=torch.float64, device=dev)
     p = _lib.ptr
+    ctx.bind_torch_stream()
     _lib.check(_lib.load().socp_pack_csc(ctx.handle, B, rows, cols, p(nz_offs), p(colptr), p(rowval),
                                          p(nzval), index_base, p(out)))
     return out[:B * rows * cols]

@@ -22,12 +22,15 @@ F_DEVICE_PTRS, F_WARM_START, F_FORCE_LARGE = 1, 2, 4
 
 EXPORTED = [
     "socp_last_error", "socp_version", "socp_params_default", "socp_ctx_create",
-    "socp_ctx_destroy", "socp_ctx_sync", "socp_ctx_stream", "socp_supported",
+    "socp_ctx_destroy", "socp_ctx_sync", "socp_ctx_stream", "socp_ctx_set_stream", "socp_ctx_reset_stream", "socp_supported",
     "socp_batch_solve", "socp_batch_solve_ex", "socp_batch_kkt_solve", "socp_generate",
     "socp_last_kernel_ms", "socp_last_kernel_name", "socp_debug_set_kkt_dump",
     "socp_debug_set_stamps", "socp_pack_csc", "socp_comm_unique_id", "socp_comm_init",
-    "socp_comm_destroy", "socp_allgather_status",
+    "socp_comm_destroy", "socp_allgather_status", "socp_allgather_outcomes",
 ]
+
+OUTCOME_BYTES = 32  # sizeof(socp_outcome): int32 status, int32 iters, double rd, rp, gap
+MAX_BATCH = 2**31 - 1  # device problem indices are int32
 
 
 class SocpError(RuntimeError):
@@ -83,6 +86,8 @@ def load():
     L.socp_ctx_sync.argtypes = [vp]
     L.socp_ctx_stream.argtypes = [vp]
     L.socp_ctx_stream.restype = C.c_void_p
+    L.socp_ctx_set_stream.argtypes = [vp, vp]
+    L.socp_ctx_reset_stream.argtypes = [vp]
     L.socp_supported.argtypes = [C.POINTER(Dims)]
     common = [vp, C.POINTER(Dims), i32p, i32p, i32p]
     L.socp_batch_solve.argtypes = common + [dp] * 5 + [u8p, C.POINTER(Params)] + [dp] * 4 + [i32p, i32p]
@@ -100,6 +105,7 @@ def load():
         L.socp_comm_init.argtypes = [vp, C.c_int, C.c_int, vp, C.POINTER(C.c_void_p)]
         L.socp_comm_destroy.argtypes = [vp]
         L.socp_allgather_status.argtypes = [vp, C.c_int64, vp, vp, vp]
+        L.socp_allgather_outcomes.argtypes = [vp, C.c_int64, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -145,6 +151,22 @@ class Context:
     @property
     def stream(self) -> int:
         return load().socp_ctx_stream(self.handle)
+
+    def set_stream(self, stream) -> None:
+        """Issue the context's work on `stream` (a hipStream_t as int; 0 is the
+        null stream, torch's default) -- socp_ctx_set_stream."""
+        check(load().socp_ctx_set_stream(self.handle, C.c_void_p(stream) if stream else None))
+
+    def reset_stream(self) -> None:
+        """Back to the context's own stream (socp_ctx_reset_stream)."""
+        check(load().socp_ctx_reset_stream(self.handle))
+
+    def bind_torch_stream(self) -> None:
+        """Order the context's work on torch's current stream of its device, so
+        tensors torch produced just before a call are complete when the solver
+        reads them, and torch work issued after it sees the results."""
+        import torch
+        self.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
     def last_kernel_ms(self) -> float:
         v = C.c_float()

@@ -87,3 +87,28 @@ def test_flop_and_byte_model():
     assert abs(bench.flops_per_problem_iter(64, 16, 96) - 939.3e3) < 0.1e3
     assert abs(bench.flops_per_problem_iter(512, 64, 640) - 344.8e6) < 0.1e6
     assert abs(bench.bytes_per_problem_iter(64, 16, 96) - 63.1e3) < 0.1e3
+
+
+def test_host_arrays_are_size_checked():
+    """every array is checked against (B, n, m, k) before the C ABI
+    reads it (a short host array would be an out-of-bounds read)."""
+    from socp_amd.configs import C1
+    cfg = C1
+    B, n, m, k = 3, cfg.n, cfg.m, cfg.k
+    good = dict(c=np.zeros(B * n), A=np.zeros(B * m * n), b=np.zeros(B * m), G=np.zeros(B * k * n),
+                h=np.zeros(B * k))
+    for key, short in (("A", B * m * n - 1), ("b", B * m + 1), ("G", B * k * n - n), ("h", B * k - 1)):
+        arrs = dict(good)
+        arrs[key] = np.zeros(short)
+        with pytest.raises(ValueError, match=key):
+            S.batch_solve(cfg.cones, n, m, k, arrs["c"], arrs["A"], arrs["b"], arrs["G"], arrs["h"])
+    with pytest.raises(ValueError, match="sing"):
+        S.batch_solve(cfg.cones, n, m, k, *good.values(), sing=np.zeros(B + 1, np.uint8))
+    with pytest.raises(ValueError, match="multiple"):
+        S.batch_solve(cfg.cones, n, m, k, np.zeros(B * n + 1), *list(good.values())[1:])
+    with pytest.raises(ValueError, match="warm_z"):
+        S.batch_solve(cfg.cones, n, m, k, *good.values(),
+                      warm=(np.zeros(B * n), np.zeros(B * m), np.zeros(B * k - 2), np.zeros(B * k)))
+    with pytest.raises(ValueError, match="dz"):
+        S.batch_kkt_solve(cfg.cones, n, m, k, good["A"], good["G"], None, np.zeros(B * k), np.zeros(B * k),
+                          np.zeros(B * n), np.zeros(B * m), np.zeros(B * k + 3), np.zeros(B * k))

@@ -1,6 +1,7 @@
 """N>1 path on the CPU: world_size-2 gloo ranks shard the global problem index,
-regenerate their shard, and all-gather (status, iters).  The oracle stands in
-for the per-rank solve (CPU-only test of the sharding and the collective)."""
+regenerate their shard, and all-gather the 32-byte outcome records (status,
+iters, ||rd||, ||rp||, z's: SURVEY.md §8(e)).  The oracle stands in for the
+per-rank solve (CPU-only test of the sharding and the collective)."""
 import os
 import socket
 
@@ -46,9 +47,10 @@ def _worker(rank, world, port, total, q):
     d = O.generate(cfg.cones, hi - lo, cfg.n, cfg.m, cfg.k, cfg.seed, first_problem=lo)
     r = O.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
                       params=O.Params(maxit=40, tol=1e-5), nthreads=1)
-    out = gather_outcomes(torch.from_numpy(r["status"]), torch.from_numpy(r["iters"]))
+    out = gather_outcomes(torch.from_numpy(r["status"]), torch.from_numpy(r["iters"]),
+                          torch.from_numpy(r["res"]))
     if rank == 0:
-        q.put(out.numpy())
+        q.put({key: v.numpy() for key, v in out.items()})
     dist.barrier()
     dist.destroy_process_group()
 
@@ -70,8 +72,34 @@ def test_gloo_world2_matches_single_process(oracle):
     d = oracle.generate(cfg.cones, total, cfg.n, cfg.m, cfg.k, cfg.seed)
     r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
                            params=oracle.Params(maxit=40, tol=1e-5), nthreads=1)
-    flat = got.reshape(total, 2)
-    assert np.array_equal(flat[:, 0], r["status"]) and np.array_equal(flat[:, 1], r["iters"])
+    assert got["status"].shape == (world, total // world)
+    assert np.array_equal(got["status"].reshape(-1), r["status"])
+    assert np.array_equal(got["iters"].reshape(-1), r["iters"])
+    # residual norms travel bit-exactly (the oracle is deterministic per problem)
+    assert np.array_equal(got["res"].reshape(total, 3), r["res"])
+
+
+def test_outcome_record_layout():
+    """pack/unpack of the socp_outcome record (include/socp.h): 32 bytes, int32
+    status and iters first, then three float64."""
+    import torch
+    from socp_amd.dist import RECORD_BYTES, pack_outcomes, unpack_outcomes
+    st = torch.tensor([0, 1, 4], dtype=torch.int32)
+    it = torch.tensor([7, 40, 3], dtype=torch.int32)
+    res = torch.tensor([[1e-6, 2e-7, 3e-8], [1.5, 2.5, 3.5], [float("inf"), -0.0, 5.0]], dtype=torch.float64)
+    rec = pack_outcomes(st, it, res)
+    assert rec.shape == (3, RECORD_BYTES) and RECORD_BYTES == 32
+    raw = rec.numpy().tobytes()
+    import struct
+    for p in range(3):
+        s_, i_, a, b, c = struct.unpack_from("<iiddd", raw, 32 * p)
+        assert (s_, i_) == (int(st[p]), int(it[p]))
+        assert [a, b, c] == res[p].tolist()
+    back = unpack_outcomes(rec)
+    assert torch.equal(back["status"], st) and torch.equal(back["iters"], it)
+    assert torch.equal(back["res"], res)
+    nan = unpack_outcomes(pack_outcomes(st, it))["res"]
+    assert torch.isnan(nan).all()
 
 
 @pytest.mark.gpu
@@ -94,5 +122,20 @@ def test_abi_status_gather_single_rank():
         out = comm.allgather_status(st, it)
         assert out.shape == (1, B, 2)
         assert torch.equal(out[0, :, 0], st) and torch.equal(out[0, :, 1], it)
+        # the 32-byte record with the residual norms of a real solve
+        from socp_amd.configs import C1
+        cfg = C1
+        c, A, b, G, h = S.generate(cfg.cones, 64, cfg.n, cfg.m, cfg.k, cfg.seed, ctx=ctx)
+        o = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h,
+                          torch.zeros(64, dtype=torch.uint8, device="cuda"), maxit=40, tol=1e-5, ctx=ctx,
+                          res=True)
+        rec = comm.allgather_outcomes(o["status"], o["iters"], o["res"])
+        assert rec["status"].shape == (1, 64)
+        assert torch.equal(rec["status"][0], o["status"]) and torch.equal(rec["iters"][0], o["iters"])
+        assert torch.equal(rec["res"][0], o["res"].view(64, 3))
+        conv = o["status"] == 0
+        assert conv.any()
+        # converged problems satisfy the reference exit test (solver.jl:122)
+        assert (rec["res"][0][conv].sum(dim=1) < 1e-5).all()
     finally:
         comm.close()

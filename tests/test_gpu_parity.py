@@ -362,3 +362,91 @@ def test_pack_csc_matches_dense():
     with pytest.raises(S.SocpError) as e:
         S.pack_csc(bad, rows, cols)
     assert e.value.code == -1
+
+
+def test_warm_start_from_fresh_device_tensors(oracle):
+    """inputs torch computes just before a device-mode call (here the
+    warm-start iterate, produced by a chain of torch ops on torch's current
+    stream) are complete when the solver reads them: the context's work is
+    ordered on torch's stream (socp_ctx_set_stream)."""
+    import torch
+    cfg, B = C2, 512
+    c, A, b, G, h = S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    sing = torch.zeros(B, dtype=torch.uint8, device=G.device)
+    a2 = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=2, tol=0.0)
+    ref = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=3, tol=0.0,
+                        warm=(a2["x"], a2["y"], a2["z"], a2["s"]))
+    ref = {key: v.clone() for key, v in ref.items()}
+    for _ in range(3):
+        # a long dependent torch chain that ends in the warm iterate: x + big - big
+        big = torch.full_like(a2["z"], 1e3)
+        wz = a2["z"].clone()
+        for _ in range(50):
+            wz = (wz + big) - big + 0.0 * torch.sin(wz)
+        wz = a2["z"].clone().copy_(a2["z"])  # exact values, produced last on the stream
+        wx, wy, ws = a2["x"] * 1.0, a2["y"] * 1.0, a2["s"] * 1.0
+        got = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=3, tol=0.0,
+                            warm=(wx, wy, wz, ws))
+        # consume on torch's stream without an explicit context sync
+        assert torch.equal(got["x"], ref["x"]) and torch.equal(got["z"], ref["z"])
+
+
+def test_pack_csc_unsorted_nonadjacent_duplicates():
+    """a hand-built CSC whose column has unsorted rows with a
+    non-adjacent duplicate ([3, 5, 3]) sums both entries (device kernel), and
+    scipy input is canonicalised (sum_duplicates) before packing."""
+    import scipy.sparse as sp
+    import torch
+    rows, cols = 8, 3
+    dev = torch.device("cuda", 0)
+    i64 = dict(dtype=torch.int64, device=dev)
+    # column 0: rows [3, 5, 3] (values 1, 2, 4); column 1 empty; column 2: rows [6, 1]
+    colptr = torch.tensor([1, 4, 4, 6], **i64)  # Julia 1-based
+    rowval = torch.tensor([4, 6, 4, 7, 2], **i64)
+    nzval = torch.tensor([1.0, 2.0, 4.0, 8.0, 16.0], dtype=torch.float64, device=dev)
+    nz_offs = torch.tensor([0, 5], **i64)
+    for _ in range(5):  # the sum must not depend on which thread stores first
+        got = S.pack_csc((nz_offs, colptr, rowval, nzval), rows, cols).cpu().numpy().reshape(cols, rows).T
+        want = np.zeros((rows, cols))
+        want[3, 0], want[5, 0], want[6, 2], want[1, 2] = 5.0, 2.0, 8.0, 16.0
+        assert np.array_equal(got, want)
+    # scipy: an unsorted csc with a non-adjacent duplicate
+    m = sp.csc_matrix((np.array([1.0, 2.0, 4.0]), np.array([3, 5, 3]), np.array([0, 3, 3, 3])), shape=(rows, cols))
+    got = S.pack_csc([m]).cpu().numpy().reshape(cols, rows).T
+    assert got[3, 0] == 5.0 and got[5, 0] == 2.0 and np.count_nonzero(got) == 2
+
+
+def test_batch_above_int32_rejected():
+    """the persistent kernels index problems with an int32 counter."""
+    import ctypes as C
+    from socp_amd import _lib
+    L = _lib.load()
+    ctx = S.default_context()
+    kind, offs, dim = S.cone_arrays(C1.cones)
+    d = _lib.Dims(2**31, C1.n, C1.m, C1.k, len(kind))
+    p = _lib.ptr
+    rc = L.socp_generate(ctx.handle, C.byref(d), p(kind), p(offs), p(dim), 1, 0, None, None, None, None, None)
+    assert rc == _lib.SOCP_E_INVALID and b"2^31" in L.socp_last_error()
+    rc = L.socp_pack_csc(ctx.handle, 2**31, 4, 4, None, None, None, None, 1, None)
+    assert rc == _lib.SOCP_E_INVALID
+
+
+def test_problem_dump_env(tmp_path, monkeypatch, oracle):
+    """SOCP_DUMP_DIR mirrors the reference's commented-out dumps (solver.jl:48-67,
+    75-82): A, G, c, b, h, cones and initv = [-c; b; h] of the first problems."""
+    cfg, B = C1, 4
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    monkeypatch.setenv("SOCP_DUMP_DIR", str(tmp_path))
+    monkeypatch.setenv("SOCP_DUMP_COUNT", "2")
+    gpu_batch(dims(cfg), d, B, maxit=1, tol=0.0)
+    monkeypatch.delenv("SOCP_DUMP_DIR")
+    n, m, k = cfg.n, cfg.m, cfg.k
+    for p in range(2):
+        pc, pA, pb, pG, ph = batch_problem(d, B, n, m, k, p)
+        assert np.array_equal(np.loadtxt(tmp_path / f"problem{p}_G.txt"), pG)
+        assert np.array_equal(np.loadtxt(tmp_path / f"problem{p}_A.txt"), pA)
+        assert np.array_equal(np.loadtxt(tmp_path / f"problem{p}_h.txt"), ph)
+        iv = np.loadtxt(tmp_path / f"problem{p}_initv.txt")
+        assert np.array_equal(iv, np.concatenate([-pc, pb, ph]))
+        assert (tmp_path / f"problem{p}_cones.txt").read_text().split() == ["SOC(0,48)"]
+    assert not (tmp_path / "problem2_G.txt").exists()

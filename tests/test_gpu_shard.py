@@ -1,0 +1,117 @@
+"""C3 (BASELINE.json configs[3]: 524,288 problems sharded over 8 MI355X) on one
+GPU, one shard at a time: the last rank's shard, first_problem = 7 * 65536.
+
+A multi-GPU run gives rank r the global problems [r*B, (r+1)*B) and generates
+them on its own device from the global index, so the N=8
+job is eight of these shards plus the 32-byte outcome all-gather.  This file
+checks the shard a rank would solve at full size:
+  * size-independent properties of all 65,536 problems (finite, strictly
+    interior iterates, every problem at maxit under fixed-K);
+  * 24 sampled problems against the oracle (x <= 1e-6, z and s <= 1e-5);
+  * a 256-problem slice solved on its own at a non-zero offset inside the
+    shard is bitwise equal to the same problems inside the full shard;
+  * the shard's outcome records (status, iters, ||rd||, ||rp||, z's) match the
+    per-problem results.
+"""
+import numpy as np
+import pytest
+
+import socp_amd as S
+from socp_amd.configs import C3
+from problems import batch_problem
+
+pytestmark = pytest.mark.gpu
+
+RANK, WORLD = 7, 8
+B = C3.batch // WORLD  # 65,536 problems per rank
+K = 8  # fixed-K headline count
+
+
+def rel(a, b):
+    a = np.asarray(a).reshape(-1)
+    b = np.asarray(b).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def shard():
+    import torch
+    cfg = C3
+    first = RANK * B
+    c, A, b, G, h = S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed, first_problem=first)
+    sing = torch.zeros(B, dtype=torch.uint8, device=G.device)
+    out = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=K, tol=0.0, res=True)
+    torch.cuda.synchronize()
+    return dict(first=first, data=(c, A, b, G, h), sing=sing, out=out)
+
+
+def test_c3_last_shard_properties(shard):
+    cfg = C3
+    out = shard["out"]
+    st = out["status"].cpu().numpy()
+    assert (st == S.MAXIT).all(), np.bincount(st, minlength=5)
+    assert (out["iters"].cpu().numpy() == K).all()
+    for key in ("x", "y", "z", "s", "res"):
+        assert np.isfinite(out[key].cpu().numpy()).all(), key
+    z = out["z"].cpu().numpy().reshape(B, cfg.k)
+    s = out["s"].cpu().numpy().reshape(B, cfg.k)
+    for arr in (z, s):
+        assert (arr[:, :32] > 0).all()  # POC block
+        for o in (32, 64):
+            assert (arr[:, o] > np.linalg.norm(arr[:, o + 1:o + 32], axis=1)).all()  # SOC heads
+    res = out["res"].cpu().numpy().reshape(B, 3)
+    assert (res[:, 2] > 0).all()
+    assert np.median(res[:, 2]) < 1.0
+
+
+def test_c3_last_shard_matches_oracle(shard, oracle):
+    cfg = C3
+    out = shard["out"]
+    flat = {key: t.cpu().numpy() for key, t in zip(("c", "A", "b", "G", "h"), shard["data"])}
+    # the device generator keyed on the global index reproduces the CPU restatement
+    d0 = oracle.generate(cfg.cones, 4, cfg.n, cfg.m, cfg.k, cfg.seed, first_problem=shard["first"] + B - 4)
+    for key in ("c", "G", "h"):
+        n_el = d0[key].size // 4
+        assert np.array_equal(flat[key][(B - 4) * n_el:], d0[key]), key
+    # x within 1e-6 after K = 8 iterations (the C2 full-size gate); z and s
+    # within 1e-5: by iteration 8 kappa(H) reaches 1e6-1e8 on some problems and
+    # rounding-level differences in H^-1 (sweep vs potrs) grow into the cone
+    # iterates first
+    idx = np.random.default_rng(7).choice(B, 24, replace=False)
+    for p in idx:
+        pc, pA, pb, pG, ph = batch_problem(flat, B, cfg.n, cfg.m, cfg.k, p)
+        r = oracle.solve_trace(cfg.cones, pc, pA, pb, pG, ph, sing=False, params=oracle.Params(maxit=K, tol=0.0))
+        assert r["status"] == S.MAXIT
+        for key, dim, tol in (("x", cfg.n, 1e-6), ("z", cfg.k, 1e-5), ("s", cfg.k, 1e-5)):
+            got = out[key][p * dim:(p + 1) * dim].cpu().numpy()
+            assert rel(got, r[key]) <= tol, (p, key, rel(got, r[key]))
+
+
+def test_c3_slice_bitwise_equals_full_shard(shard):
+    """Problems first+1000 .. first+1255 solved as their own batch (generated at
+    that global offset) are bitwise the same as inside the full shard."""
+    import torch
+    cfg = C3
+    off, Bs = 1000, 256
+    c, A, b, G, h = S.generate(cfg.cones, Bs, cfg.n, cfg.m, cfg.k, cfg.seed, first_problem=shard["first"] + off)
+    full = shard["data"]
+    n, m, k = cfg.n, cfg.m, cfg.k
+    for got, ref, per in zip((c, A, b, G, h), full, (n, m * n, m, k * n, k)):
+        assert torch.equal(got, ref[off * per:(off + Bs) * per])
+    sing = torch.zeros(Bs, dtype=torch.uint8, device=G.device)
+    one = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=0.0, res=True)
+    torch.cuda.synchronize()
+    out = shard["out"]
+    for key, per in (("x", n), ("y", m), ("z", k), ("s", k), ("res", 3)):
+        assert torch.equal(one[key], out[key][off * per:(off + Bs) * per]), key
+    assert torch.equal(one["status"], out["status"][off:off + Bs])
+
+
+def test_c3_outcome_records(shard):
+    """The 32-byte records the shard contributes to the all-gather."""
+    import torch
+    from socp_amd.dist import pack_outcomes, unpack_outcomes
+    out = shard["out"]
+    rec = unpack_outcomes(pack_outcomes(out["status"], out["iters"], out["res"]))
+    assert torch.equal(rec["status"], out["status"]) and torch.equal(rec["iters"], out["iters"])
+    assert torch.equal(rec["res"], out["res"].view(B, 3))

@@ -162,3 +162,21 @@ def test_fixed_k_mode(oracle):
     r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
                            params=oracle.Params(maxit=3, tol=0.0))
     assert (r["status"] == 1).all() and (r["iters"] == 3).all()
+
+
+def test_structured_mode_matches_reference_order(oracle):
+    """The oracle's structured mode (X = W^-1 G per cone, H = X'X, no dense iWiW:
+    the algorithm the kernels run; bench.py times it as the second CPU line)
+    agrees with the reference op order inside the healthy window."""
+    import numpy as np
+    from socp_amd.configs import C1, C2
+    for cfg, K in ((C1, 3), (C2, 6)):
+        B = 16
+        d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+        args = (cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"])
+        r = oracle.batch_solve(*args, sing=np.zeros(B, np.uint8), params=oracle.Params(maxit=K, tol=0.0))
+        s = oracle.batch_solve(*args, sing=np.zeros(B, np.uint8),
+                               params=oracle.Params(maxit=K, tol=0.0, flags=oracle.F_STRUCTURED))
+        assert (r["status"] == s["status"]).all()
+        for key in ("x", "z", "s"):
+            assert np.linalg.norm(r[key] - s[key]) <= 1e-9 * np.linalg.norm(r[key]), (cfg.name, key)
