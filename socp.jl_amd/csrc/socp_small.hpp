@@ -75,41 +75,41 @@ enum : int {
   O_CDIM = O_COFF + NCS,     // cone dim[NCS]
   O_CKIND = O_CDIM + NCS,    // cone kind[NCS]
   O_CC = O_CKIND + NCS,        // per-cone constants of the current scaling [NCC][NCS]
-  O_PART = O_CC + 12 * NCS,    // segment partials [NVMAX][NCS][2 slots] (zero where unused)
-  O_TOTC = O_PART + 4 * NCS * 2,  // per-cone results [2][NCS]
-  O_STAMPS = O_TOTC + 2 * NCS,  // diagnostic build: per-phase cycle totals of this wave [24]
-  O_KV = O_STAMPS + 24         // 16 k-vectors, Shape::KS apart
+  O_PART = O_CC + 20 * NCS,    // segment partials [NVMAX = 6][NCS][2 slots] (zero where unused)
+  O_TOTC = O_PART + 6 * NCS * 2,  // per-cone results [4][NCS]
+  O_STAMPS = O_TOTC + 4 * NCS,  // diagnostic build: per-phase cycle totals of this wave [24]
+  O_KV = O_STAMPS + 24         // 17 k-vectors, Shape::KS apart
 };
+constexpr int NKV = 17;
 // per-cone constants (SOC cones), recomputed by every scaling:
 //   MU = mu, IMU = 1/mu, WB0 = wbar_0, I1 = 1/(1+wbar_0), W2 = |wbar_1|^2,
 //   L0 = lambda_0, AA = lambda_0^2 - |lambda_1|^2 (iprod!'s `a`, vectors.jl:105),
 //   IAA = 1/AA, IL0 = 1/lambda_0, IL0AA = 1/(lambda_0 AA),
-//   SA = 1/sqrt(AA) (scmax's `a`, mats.jl:66), SAL = 1/(SA lambda_0 + 1)
+//   SA = 1/sqrt(AA) (scmax's `a`, mats.jl:66), SAL = 1/(SA lambda_0 + 1),
+//   WL = wbar_1'lambda_1; AS, AZ, BS, BZ: the tail rows of wbar and lambda as
+//   wbar_i = AS s_i - AZ z_i, lambda_i = BS s_i + BZ z_i (scalings.jl:57-97);
+// per solve: DLT = wbar_1'k0_1 of the current KKT solve's k0 (solve_head ->
+// solve_tail), KK = the cone's kt2'kt3 (head of kt2 o kt3, solve_tail -> affine_post)
 enum : int { CC_MU, CC_IMU, CC_WB0, CC_I1, CC_W2, CC_L0, CC_AA, CC_IAA, CC_IL0, CC_IL0AA, CC_SA,
-             CC_SAL };
+             CC_SAL, CC_WL, CC_AS, CC_AZ, CC_BS, CC_BZ, CC_DLT, CC_KK };
 __host__ __device__ constexpr int cc(int q, int c) { return O_CC + q * NCS + c; }
-// k-vector ids
+// k-vector ids (IL: 1/lambda_i of the POC elements)
 enum : int { KV_H, KV_Z, KV_S, KV_DZ, KV_DS, KV_RZ, KV_RS, KV_LAM, KV_WB, KV_CA, KV_CB, KV_K0,
-             KV_K1, KV_K2, KV_T1, KV_T2 };
+             KV_K1, KV_K2, KV_T1, KV_T2, KV_IL };
 
 template <int NQ, int NP, int MQ>
 struct Shape {
   static constexpr int NPAD = 16 * NQ, KP = 4 * NP, MPAD = 16 * MQ, LDA = NPAD + 1;
-  // k-vector stride: a shape whose k-vectors fit slot 0 (KP <= 64) packs them
-  // KP apart (C1: 20 KiB of LDS per wave, so 8 waves fit a CU).  Lanes read
-  // slot 1 / padding elements i >= KP unconditionally and mask the values by
-  // their type code (3 = pad), so those reads may alias the next vector; every
+  // k-vector stride KP: lanes read slot 1 / padding elements i >= KP
+  // unconditionally and mask the values by their type code (3 = pad), so those
+  // reads may alias the next vector (the last one reads into the A block); every
   // write is guarded by i < k or the code, and rows [k, KP) stay zero.
-  static constexpr int KS = KP > 64 ? KMAX : KP;
-  // sweep gather buffer: pivot column of the diagonal tile [16] + pivot row of
-  // every tile of the panel slab [16 per tile]
-  static constexpr int CB = 16 + (NPAD > MPAD ? NPAD : MPAD);
-  static constexpr int O_A = O_KV + 16 * KS;
+  static constexpr int KS = KP;
+  static constexpr int O_A = O_KV + NKV * KS;
   static constexpr int O_NV = O_A + MPAD * LDA;    // n-vectors: c x rd rx n0 tn
   static constexpr int O_MV = O_NV + 6 * NPAD;     // m-vectors: b y rp ry m0 tm
   static constexpr int O_U = O_MV + 6 * MPAD;      // U[NCS][NPAD]
-  static constexpr int O_COL = O_U + NCS * NPAD;   // sweep column buffers [2][CB]
-  static constexpr int O_TB = O_COL + 2 * CB;      // tile transpose [16][17]
+  static constexpr int O_TB = O_U + NCS * NPAD;    // tile transpose [16][17]
   static constexpr int TOTAL = O_TB + 16 * 17;
   static constexpr int nv(int id) { return O_NV + id * NPAD; }
   static constexpr int mv(int id) { return O_MV + id * MPAD; }
@@ -118,9 +118,9 @@ enum : int { NV_C, NV_X, NV_RD, NV_RX, NV_N0, NV_TN };
 enum : int { MV_B, MV_Y, MV_RP, MV_RY, MV_M0, MV_TM };
 
 inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
-  int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = NPAD + 1, CB = 16 + (NPAD > MPAD ? NPAD : MPAD);
-  int KS = 4 * NP > 64 ? KMAX : 4 * NP;  // Shape::KS
-  int total = O_KV + 16 * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + NCS * NPAD + 2 * CB + 16 * 17;
+  int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = NPAD + 1;
+  int KS = 4 * NP;  // Shape::KS
+  int total = O_KV + NKV * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + NCS * NPAD + 16 * 17;
   return (size_t)total * sizeof(double);
 }
 
@@ -145,6 +145,16 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
 #endif
 enum { SP_LOAD, SP_SCALING, SP_RESID, SP_U, SP_SYRK, SP_SWEEP_H, SP_SCHUR, SP_SOLVE, SP_STEP, SP_VOP,
        SP_STORE, SP_OTHER };
+
+// Static-analysis build (-DSOCP_MARK, tools/isa_phases.py): region markers as
+// assembly comments; never in a product or diagnostic library.
+#ifdef SOCP_MARK
+#define MARK_BEGIN(name) asm volatile(";@@BEGIN " name)
+#define MARK_END(name) asm volatile(";@@END " name)
+#else
+#define MARK_BEGIN(name) do {} while (0)
+#define MARK_END(name) do {} while (0)
+#endif
 
 extern __shared__ double socp_lds[];
 #define LDS(i) socp_lds[(i)]
@@ -373,7 +383,7 @@ struct Small {
   static constexpr int NT = NQ * (NQ + 1) / 2;
   static constexpr int MT = MQ * (MQ + 1) / 2;
   static constexpr int NPAD = SH::NPAD, KP = SH::KP, MPAD = SH::MPAD, LDA = SH::LDA;
-  static constexpr int O_A = SH::O_A, O_U = SH::O_U, O_COL = SH::O_COL, O_TB = SH::O_TB;
+  static constexpr int O_A = SH::O_A, O_U = SH::O_U, O_TB = SH::O_TB;
   static constexpr int C_ = SH::nv(NV_C), X_ = SH::nv(NV_X), RD = SH::nv(NV_RD),
                        RX = SH::nv(NV_RX), N0 = SH::nv(NV_N0), TN = SH::nv(NV_TN);
   static constexpr int B_ = SH::mv(MV_B), Y_ = SH::mv(MV_Y), RP = SH::mv(MV_RP),
@@ -382,7 +392,8 @@ struct Small {
   static constexpr int H_ = kvs(KV_H), Z_ = kvs(KV_Z), S_ = kvs(KV_S), DZ = kvs(KV_DZ),
                        DS = kvs(KV_DS), RZ = kvs(KV_RZ), RS = kvs(KV_RS), LAM = kvs(KV_LAM),
                        WB = kvs(KV_WB), CA = kvs(KV_CA), CBV = kvs(KV_CB), K0 = kvs(KV_K0),
-                       K1 = kvs(KV_K1), K2 = kvs(KV_K2), T1 = kvs(KV_T1), T2 = kvs(KV_T2);
+                       K1 = kvs(KV_K1), K2 = kvs(KV_K2), T1 = kvs(KV_T1), T2 = kvs(KV_T2),
+                       IL = kvs(KV_IL);
 
   const SmallArgs& a;
   const int lane, g, cl;
@@ -449,6 +460,7 @@ struct Small {
   }
 
   __device__ __forceinline__ void load_problem(int64_t p) {
+    MARK_BEGIN("load_problem");
     LANE_IDS();
     const double* Gp = a.G + p * (int64_t)k * n;
     // G -> AGPRs.  a_put is an asm statement the scheduler does not move loads
@@ -487,8 +499,8 @@ struct Small {
     double av[AB];
 #pragma unroll
     for (int t = 0; t < AB; ++t) av[t] = (64 * t + lane < mn) ? Ap[64 * t + lane] : 0.0;
-    for (int e = lane; e < 16 * SH::KS; e += 64) LDS(O_KV + e) = 0.0;
-    for (int e = lane; e < SH::O_COL - O_A; e += 64) LDS(O_A + e) = 0.0;
+    for (int e = lane; e < NKV * SH::KS; e += 64) LDS(O_KV + e) = 0.0;
+    for (int e = lane; e < SH::O_TB - O_A; e += 64) LDS(O_A + e) = 0.0;
     SYNC();
     if (lane < n) LDS(C_ + lane) = cv;
     if (lane < m) LDS(B_ + lane) = bv;
@@ -523,6 +535,7 @@ struct Small {
       LDS(LAM + i) = e;
       LDS(CA + i) = 1.0;
       LDS(CBV + i) = 0.0;
+      LDS(IL + i) = e;  // 1/lambda_i of the POC elements (lambda = e)
     }
     for (int e = lane; e < NCS * NPAD; e += 64) LDS(O_U + e) = 0.0;
     if (lane < nc) {  // W = I, lambda = e: mu = wbar_0 = lambda_0 = 1, wbar_1 = lambda_1 = 0
@@ -539,6 +552,7 @@ struct Small {
       LDS(cc(CC_IL0AA, c)) = 1.0;
       LDS(cc(CC_SA, c)) = 1.0;
       LDS(cc(CC_SAL, c)) = 0.5;
+      LDS(cc(CC_WL, c)) = 0.0;
     }
     SYNC();
   }
@@ -562,6 +576,7 @@ struct Small {
   // predicate); all partials are read before any is used.
   template <int NV, unsigned MX>
   __device__ __forceinline__ void cone_reduce(double (&v)[2][NV]) {
+    MARK_BEGIN("cone_reduce");
     LANE_IDS();
     constexpr int NS = KP > 64 ? 2 : 1;  // slots that can hold elements of this shape
     const int rl = lane & 15;
@@ -608,6 +623,45 @@ struct Small {
       }
   }
 
+  // The scan half of cone_reduce for sums: the segment-end lanes leave the
+  // two slot partials of every cone in O_PART; cone_tot(q, c) adds them (the
+  // unused (cone, slot) entries stay zero).  For per-cone work done once per
+  // cone (on "cone lanes", lane c < nc) instead of once per element.
+  template <int NV>
+  __device__ __forceinline__ void cone_partials(double (&v)[2][NV]) {
+    MARK_BEGIN("cone_partials");
+    LANE_IDS();
+    constexpr int NS = KP > 64 ? 2 : 1;
+    const int rl = lane & 15;
+#define SOCP_SCAN_STEP(CTRL, OK)                         \
+  _Pragma("unroll") for (int s = 0; s < NS; ++s) {       \
+    const int st = ssl[s];                               \
+    const bool ok_ = (OK);                               \
+    _Pragma("unroll") for (int q = 0; q < NV; ++q) {     \
+      const double y = dpp_all<CTRL>(v[s][q]);           \
+      v[s][q] = ok_ ? v[s][q] + y : v[s][q];             \
+    }                                                    \
+  }
+    SOCP_SCAN_STEP(0x111, rl >= 1 && lane - 1 >= st)
+    SOCP_SCAN_STEP(0x112, rl >= 2 && lane - 2 >= st)
+    SOCP_SCAN_STEP(0x114, rl >= 4 && lane - 4 >= st)
+    SOCP_SCAN_STEP(0x118, rl >= 8 && lane - 8 >= st)
+    SOCP_SCAN_STEP(0x142, ((lane >> 4) & 1) && ((lane & ~15) - 1 >= st))
+    SOCP_SCAN_STEP(0x143, lane >= 32 && 31 >= st)
+#undef SOCP_SCAN_STEP
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (lane == sle[s]) {
+#pragma unroll
+        for (int q = 0; q < NV; ++q) LDS(O_PART + (q * NCS + ci[s]) * 2 + s) = v[s][q];
+      }
+    }
+    SYNC();
+  }
+  __device__ __forceinline__ double cone_tot(int q, int c) const {
+    return LDS(O_PART + (q * NCS + c) * 2) + LDS(O_PART + (q * NCS + c) * 2 + 1);
+  }
+
   __device__ __forceinline__ double ccv(int q, int c) const { return LDS(cc(q, c)); }
 
   // max over cones of the value the first lane of every cone stored at O_TOTC + off
@@ -617,262 +671,299 @@ struct Small {
     return t;
   }
 
+  // reciprocal and reciprocal square root: hardware estimate + Newton steps
+  // (within an ulp or two of the IEEE quotient: the parity gates are relative
+  // 1e-9, and these replace IEEE divisions in per-element and per-cone math)
+  __device__ __forceinline__ static double rcp_nr(double d) { return recip(d); }
+
   // compute_scaling (scalings.jl:22-110) and ds = lam o lam (solver.jl:120).
-  // Writes WB (wbar / sqrt(s/z)), LAM, the X = W^-1 G row coefficients CA, CBV,
-  // DS (write_ds: the iteration's lam o lam; the KKT entry keeps its ds), and the
-  // per-cone constants; ll = lam'lam.  Returns the DomainError flag;
-  // dm_aa flags a negative lambda_0^2 - |lambda_1|^2 (scmax's sqrt, mats.jl:66),
-  // which the reference raises later, at compute_step.
+  // Writes WB (wbar / sqrt(s/z)), LAM, IL (1/lambda of the POC elements), the
+  // X = W^-1 G row coefficients CA, CBV, DS (write_ds: the iteration's
+  // lam o lam; the KKT entry keeps its ds) and the per-cone constants; ll =
+  // lam'lam.  Returns the DomainError flag; dm_aa flags a negative
+  // lambda_0^2 - |lambda_1|^2 (scmax's sqrt, mats.jl:66), which the reference
+  // raises later, at compute_step.
+  // Two segmented reductions; the SOC cone math (norms, gamma, mu, lambda_0 and
+  // the coefficients of the tail rows) runs once per cone on lane c, not once
+  // per element.
   __device__ __forceinline__ bool scaling_op(double& ll, bool& dm_aa, bool write_ds) {
+    MARK_BEGIN("scaling_op");
     LANE_IDS();
-    double v[2][3], zi[2], si[2], z0[2], s0[2];
+    double v[2][3], zi[2], si[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int i = 64 * s + lane, o = eo[s];
+      const int i = 64 * s + lane;
       zi[s] = LDS(Z_ + i);
       si[s] = LDS(S_ + i);
-      z0[s] = LDS(Z_ + o);
-      s0[s] = LDS(S_ + o);
       const bool tail = kd[s] == 2;
       v[s][0] = tail ? zi[s] * zi[s] : 0.0;
       v[s][1] = tail ? si[s] * si[s] : 0.0;
       v[s][2] = tail ? zi[s] * si[s] : 0.0;
     }
-    cone_reduce<3, 0>(v);
+    cone_partials<3>(v);
+    MARK_BEGIN("scal_cone1");
     bool dm = false;
-    double li[2], wbi[2], l0v[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      li[s] = wbi[s] = l0v[s] = 0.0;
-      if (64 * s >= k) continue;
-      const int i = 64 * s + lane, c = ci[s];
-      const bool hd = kd[s] == 1, poc = kd[s] == 0, real = kd[s] != 3;
-      // POC (scalings.jl:22-30)
-      const double r = si[s] / zi[s], pr = si[s] * zi[s], ir = zi[s] / si[s];
-      const bool dp = (r < 0.0) || (pr < 0.0) || (ir < 0.0);
-      // SOC (scalings.jl:32-99)
-      const double onrmz = z0[s] * z0[s] - v[s][0], onrms = s0[s] * s0[s] - v[s][1];
+    // ---- cone lanes: the SOC branch of compute_scaling (scalings.jl:32-99)
+    if (lane < nc && (int)LDS(O_CKIND + lane) == SOC_K) {
+      const int c = lane, o = (int)LDS(O_COFF + c);
+      const double z0 = LDS(Z_ + o), s0 = LDS(S_ + o);
+      const double onrmz = z0 * z0 - cone_tot(0, c), onrms = s0 * s0 - cone_tot(1, c);
       const double nrmz = sqrt(onrmz), nrms = sqrt(onrms);
       const double fz = 1.0 / nrmz, fs = 1.0 / nrms;
-      const double zb0 = z0[s] * fz, sb0 = s0[s] * fs;
-      const double nsum = zb0 * sb0 + v[s][2] * fz * fs;
+      const double zb0 = z0 * fz, sb0 = s0 * fs;
+      const double nsum = zb0 * sb0 + cone_tot(2, c) * fz * fs;
       const double garg = (1.0 + nsum) / 2.0;
       const double gamma = sqrt(garg);
       const double fg = 1.0 / (2.0 * gamma);
       const double wb0 = (sb0 + zb0) * fg;
-      const double zbi = zi[s] * fz, sbi = si[s] * fs;
       const double ratio = nrms / nrmz, prod = nrms * nrmz;
-      const double mu = sqrt(ratio);
-      const double tmv1 = sqrt(prod);
+      const double mu = sqrt(ratio), tmv1 = sqrt(prod);
       const double mult = tmv1 / (zb0 + sb0 + 2.0 * gamma);
       const double l0 = gamma * tmv1;
       const double im = 1.0 / mu;
-      const bool ds_ = (onrmz < 0.0) || (onrms < 0.0) || (garg < 0.0) || (ratio < 0.0) || (prod < 0.0);
-      const double wsoc = hd ? wb0 : (sbi - zbi) * fg;
-      const double lsoc = hd ? l0 : (sbi * (gamma + zb0) + zbi * (gamma + sb0)) * mult;
-      dm |= real && (poc ? dp : ds_);
-      wbi[s] = poc ? sqrt(r) : wsoc;
-      li[s] = poc ? sqrt(pr) : lsoc;
-      l0v[s] = l0;
-      if (real) {
+      dm = (onrmz < 0.0) || (onrms < 0.0) || (garg < 0.0) || (ratio < 0.0) || (prod < 0.0);
+      LDS(cc(CC_MU, c)) = mu;
+      LDS(cc(CC_IMU, c)) = im;
+      LDS(cc(CC_WB0, c)) = wb0;
+      LDS(cc(CC_I1, c)) = 1.0 / (1.0 + wb0);
+      LDS(cc(CC_L0, c)) = l0;
+      LDS(cc(CC_AS, c)) = fs * fg;  // wbar_i = (s_i/|s| - z_i/|z|) / (2 gamma)
+      LDS(cc(CC_AZ, c)) = fz * fg;
+      LDS(cc(CC_BS, c)) = fs * (gamma + zb0) * mult;  // lambda_i (scalings.jl:91-97)
+      LDS(cc(CC_BZ, c)) = fz * (gamma + sb0) * mult;
+      LDS(WB + o) = wb0;
+      LDS(LAM + o) = l0;
+      LDS(CA + o) = -im;
+      LDS(CBV + o) = -(1.0 + wb0) * im;
+    }
+    SYNC();
+    MARK_BEGIN("scal_elem");
+    // ---- elements: POC (scalings.jl:22-30) and the SOC tails
+    double li[2], wbi[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane, c = ci[s];
+      const bool poc = kd[s] == 0, tail = kd[s] == 2;
+      // POC: one 1/sqrt(s z) gives sqrt(s/z) = s q, sqrt(z/s) = z q, sqrt(s z) = (s z) q
+      const double pr = si[s] * zi[s];
+      const double q = rsqrt_nr(pr);
+      const double as = ccv(CC_AS, c), az = ccv(CC_AZ, c), bs = ccv(CC_BS, c), bz = ccv(CC_BZ, c);
+      const double imu = ccv(CC_IMU, c), l0 = ccv(CC_L0, c);
+      const double wt = si[s] * as - zi[s] * az;
+      const double lt = si[s] * bs + zi[s] * bz;
+      dm = dm || (poc && pr < 0.0);
+      wbi[s] = poc ? si[s] * q : (tail ? wt : ccv(CC_WB0, c));
+      li[s] = poc ? pr * q : (tail ? lt : l0);
+      if (poc || tail) {
         LDS(WB + i) = wbi[s];
         LDS(LAM + i) = li[s];
-        LDS(CA + i) = poc ? sqrt(ir) : (hd ? -im : im);
-        LDS(CBV + i) = poc ? 0.0 : (hd ? -(1.0 + wb0) * im : wsoc * im);
+        LDS(CA + i) = poc ? zi[s] * q : imu;
+        LDS(CBV + i) = poc ? 0.0 : wt * imu;
+        if (poc) LDS(IL + i) = q;
+        if (write_ds) LDS(DS + i) = poc ? li[s] * li[s] : (l0 * li[s] + l0 * li[s]);
       }
-      if (hd) {
-        LDS(cc(CC_MU, c)) = mu;
-        LDS(cc(CC_IMU, c)) = im;
-        LDS(cc(CC_WB0, c)) = wb0;
-        LDS(cc(CC_I1, c)) = 1.0 / (1.0 + wb0);
-      }
+      // lam o lam head (vprod!, vectors.jl:58-75) and |lambda_1|^2 (POC: the
+      // cone's sum of lambda_i^2, its share of lam'lam), |wbar_1|^2, wbar_1'lambda_1
+      v[s][0] = (poc || tail) ? li[s] * li[s] : 0.0;
+      v[s][1] = tail ? wbi[s] * wbi[s] : 0.0;
+      v[s][2] = tail ? wbi[s] * li[s] : 0.0;
     }
-    // lam o lam (vprod!, vectors.jl:58-75), |lam_1|^2 (iprod!'s a), |wbar_1|^2
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bool tail = kd[s] == 2;
-      v[s][0] = kd[s] != 3 ? li[s] * li[s] : 0.0;
-      v[s][1] = tail ? li[s] * li[s] : 0.0;
-      v[s][2] = tail ? wbi[s] * wbi[s] : 0.0;
-    }
-    cone_reduce<3, 0>(v);
+    cone_partials<3>(v);
+    MARK_BEGIN("scal_cone2");
     bool da = false;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (64 * s >= k) continue;
-      const int i = 64 * s + lane, c = ci[s];
-      const bool hd = kd[s] == 1, poc = kd[s] == 0;
-      const double l0 = l0v[s];
-      if (write_ds && kd[s] != 3) LDS(DS + i) = poc ? li[s] * li[s] : (hd ? v[s][0] : l0 * li[s] + l0 * li[s]);
-      if (i == eo[s] && kd[s] != 3) LDS(O_TOTC + c) = v[s][0];
-      if (hd) {
-        const double aa = l0 * l0 - v[s][1];
-        da |= aa < 0.0;
+    double tl = 0.0;
+    if (lane < nc) {
+      const int c = lane;
+      const double l1 = cone_tot(0, c);
+      if ((int)LDS(O_CKIND + c) == SOC_K) {
+        const int o = (int)LDS(O_COFF + c);
+        const double l0 = LDS(cc(CC_L0, c));
+        const double aa = l0 * l0 - l1;
+        da = aa < 0.0;
         const double sa = 1.0 / sqrt(aa);
-        LDS(cc(CC_W2, c)) = v[s][2];
-        LDS(cc(CC_L0, c)) = l0;
+        LDS(cc(CC_W2, c)) = cone_tot(1, c);
+        LDS(cc(CC_WL, c)) = cone_tot(2, c);
         LDS(cc(CC_AA, c)) = aa;
         LDS(cc(CC_IAA, c)) = 1.0 / aa;
         LDS(cc(CC_IL0, c)) = 1.0 / l0;
         LDS(cc(CC_IL0AA, c)) = 1.0 / (l0 * aa);
         LDS(cc(CC_SA, c)) = sa;
         LDS(cc(CC_SAL, c)) = 1.0 / (sa * l0 + 1.0);
+        tl = l0 * l0 + l1;
+        if (write_ds) LDS(DS + o) = tl;
+      } else {
+        tl = l1;
       }
     }
     SYNC();
-    double t = 0.0;
-    for (int c = 0; c < nc; ++c) t += LDS(O_TOTC + c);
-    ll = t;
+    ll = wsum(tl);
     dm_aa = __any(da);
     return __any(dm);
   }
 
   // First half of solve_kkt(::DenseSolver) (densesolver.jl:61-66):
   //   k0 = lam^-1 o ds (iprod!), k1 = W k0 (scale!), k2 = dz - k1,
-  //   t2 = iWiW k2 = W^-1 (W^-1 k2): the second W^-1 reuses the first one's
-  //   cone reduction (wbar_1'(W^-1 x)_1 follows from wbar_1'x_1 and |wbar_1|^2).
-  // In: DS, DZ.  Out: K0, K2, T2.
+  //   t2 = iWiW k2 = W^-1 (W^-1 k2).
+  // Every SOC dot product the chain needs follows by linearity from three dots
+  // of the inputs, taken in ONE reduction: t = lambda_1'ds_1 (iprod!'s),
+  // u = wbar_1'ds_1, w = wbar_1'dz_1, with the scaling's wbar_1'lambda_1 and
+  // |wbar_1|^2:  wbar_1'k0_1 = -ds_0 WL/aa + u/lambda_0 + WL t/(lambda_0 aa),
+  // wbar_1'k1_1 = mu (delta + (k0_0 + delta/(1+wbar_0)) |wbar_1|^2), and the
+  // second W^-1 reuses the first one's dot.  POC: k0 = ds / lambda by the
+  // reciprocal kept in IL.  In: DS, DZ.  Out: K0, K2, T2, DLT (per cone).
   __device__ __forceinline__ void solve_head() {
+    MARK_BEGIN("solve_head");
     LANE_IDS();
-    double v[2][1], x[2], lam[2], wb[2], x0[2];
+    double v[2][3], x[2], x0[2], dz[2], dz0[2], lam[2], wb[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int i = 64 * s + lane;
       x[s] = LDS(DS + i);
       x0[s] = LDS(DS + eo[s]);
+      dz[s] = LDS(DZ + i);
+      dz0[s] = LDS(DZ + eo[s]);
       lam[s] = LDS(LAM + i);
       wb[s] = LDS(WB + i);
-      v[s][0] = kd[s] == 2 ? lam[s] * x[s] : 0.0;
+      const bool tail = kd[s] == 2;
+      v[s][0] = tail ? lam[s] * x[s] : 0.0;
+      v[s][1] = tail ? wb[s] * x[s] : 0.0;
+      v[s][2] = tail ? wb[s] * dz[s] : 0.0;
     }
-    cone_reduce<1, 0>(v);
-    double k0[2], k00[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = ci[s];
-      const double t = v[s][0];
-      k00[s] = (x0[s] * ccv(CC_L0, c) - t) * ccv(CC_IAA, c);
-      const double tl = -(x0[s] * lam[s] * ccv(CC_IAA, c)) + x[s] * ccv(CC_IL0, c) + lam[s] * t * ccv(CC_IL0AA, c);
-      k0[s] = kd[s] == 0 ? x[s] / lam[s] : (kd[s] == 1 ? k00[s] : tl);
-      v[s][0] = kd[s] == 2 ? wb[s] * k0[s] : 0.0;
-    }
-    cone_reduce<1, 0>(v);
-    double k2[2], k20[2];
+    cone_reduce<3, 0>(v);
+    MARK_BEGIN("head_post");
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int i = 64 * s + lane, c = ci[s];
-      const double del = v[s][0], mu = ccv(CC_MU, c), wb0 = ccv(CC_WB0, c);
-      const double k10 = mu * (wb0 * k00[s] + del);
-      const double k1 = kd[s] == 0 ? wb[s] * k0[s] : (kd[s] == 1 ? k10 : mu * (k0[s] + (k00[s] + del * ccv(CC_I1, c)) * wb[s]));
-      k2[s] = LDS(DZ + i) - k1;
-      k20[s] = LDS(DZ + eo[s]) - k10;
-      if (kd[s] != 3) {
-        LDS(K0 + i) = k0[s];
-        LDS(K2 + i) = k2[s];
-      }
-      v[s][0] = kd[s] == 2 ? wb[s] * k2[s] : 0.0;
-    }
-    cone_reduce<1, 0>(v);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int i = 64 * s + lane, c = ci[s];
-      const double a1 = v[s][0], im = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
-      const double cy = a1 * i1 - k20[s];
-      const double y0 = im * (wb0 * k20[s] - a1);
-      const double y = kd[s] == 1 ? y0 : im * (k2[s] + cy * wb[s]);
-      const double a2 = im * (a1 + cy * ccv(CC_W2, c));
-      const double zs = kd[s] == 1 ? im * (wb0 * y0 - a2) : im * (y + (a2 * i1 - y0) * wb[s]);
+      const double t = v[s][0], u = v[s][1], w = v[s][2];
+      const double l0 = ccv(CC_L0, c), iaa = ccv(CC_IAA, c), il0 = ccv(CC_IL0, c), il0aa = ccv(CC_IL0AA, c);
+      const double mu = ccv(CC_MU, c), imu = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
+      const double w2 = ccv(CC_W2, c), wl = ccv(CC_WL, c);
+      // iprod! (vectors.jl:105-125)
+      const double k00 = (x0[s] * l0 - t) * iaa;
+      const double k0t = -(x0[s] * lam[s] * iaa) + x[s] * il0 + lam[s] * t * il0aa;
+      const double dlt = -(x0[s] * wl * iaa) + u * il0 + wl * t * il0aa;  // wbar_1'k0_1
+      // scale! (scalings.jl:159-165)
+      const double k10 = mu * (wb0 * k00 + dlt);
+      const double k1t = mu * (k0t + (k00 + dlt * i1) * wb[s]);
+      const double k20 = dz0[s] - k10;
+      const double a1 = w - mu * (dlt + (k00 + dlt * i1) * w2);  // wbar_1'k2_1
+      // iscale! twice (scalings.jl:167-173)
+      const double cy = a1 * i1 - k20;
+      const double y0 = imu * (wb0 * k20 - a1);
+      const double a2 = imu * (a1 + cy * w2);
+      // POC: elementwise, with 1/lambda and 1/w = CA
+      const double k0p = x[s] * LDS(IL + i);
+      const double k2p = dz[s] - wb[s] * k0p;
       const double ca = LDS(CA + i);
-      if (kd[s] != 3) LDS(T2 + i) = kd[s] == 0 ? ca * (ca * k2[s]) : zs;
+      const bool poc = kd[s] == 0, hd = kd[s] == 1;
+      const double k0 = poc ? k0p : (hd ? k00 : k0t);
+      const double k2 = poc ? k2p : dz[s] - (hd ? k10 : k1t);
+      const double yt = imu * (k2 + cy * wb[s]);
+      const double zs = hd ? imu * (wb0 * y0 - a2) : imu * (yt + (a2 * i1 - y0) * wb[s]);
+      if (kd[s] != 3) {
+        LDS(K0 + i) = k0;
+        LDS(K2 + i) = k2;
+        LDS(T2 + i) = poc ? ca * (ca * k2p) : zs;
+      }
+      if (hd) LDS(cc(CC_DLT, c)) = dlt;
     }
     SYNC();
   }
 
   // Second half of solve_kkt (densesolver.jl:83-88): cz = iWiW k1 = W^-1 (W^-1 k1),
-  // k0 -= W cz (W cz = W^-1 k1), cs = W k0.  With do_step, compute_step
-  // (mats.jl:30-40) of the direction (solver.jl:128-130, 143-145) follows:
-  // kt3 = W rz and kt2 = W^-1 rs are W^-1 k1 and the updated k0 exactly, so they
-  // are taken from here.  In: K1 (= G cx - k2), K0.  Out: RZ, RS, and with
-  // do_step T1 = kt3, K0 = kt2, the step length (dom: DomainError).
+  // k0 -= W cz (W cz = W^-1 k1 = y), cs = W k0.  wbar_1'(k0 - y)_1 is DLT
+  // (solve_head's) minus wbar_1'y_1, so cs needs no reduction of its own.
+  // With do_step, compute_step (mats.jl:30-40) of the direction
+  // (solver.jl:128-130, 143-145) follows: kt3 = W rz and kt2 = W^-1 rs are y
+  // and k0 - y exactly; and the dot kt2'kt3 (rho's, solver.jl:132) and each
+  // cone's kt2'kt3 (the head of kt2 o kt3, :136) come out of the step's
+  // reduction.  In: K1 (= G cx - k2), K0.  Out: RZ, RS, and with do_step
+  // T1 = kt3, K0 = kt2, KK (per cone), O_TOTC[1][0] = kt2'kt3, the step
+  // length (dom: DomainError).
   __device__ __forceinline__ double solve_tail(bool do_step, bool dm_aa, int& dom) {
+    MARK_BEGIN("solve_tail");
     LANE_IDS();
-    double v[2][1], k1[2], k10[2], wb[2];
+    double v[2][3], k1[2], k10[2], k0[2], k00[2], wb[2], lam[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int i = 64 * s + lane;
       k1[s] = LDS(K1 + i);
       k10[s] = LDS(K1 + eo[s]);
+      k0[s] = LDS(K0 + i);
+      k00[s] = LDS(K0 + eo[s]);
       wb[s] = LDS(WB + i);
-      v[s][0] = kd[s] == 2 ? wb[s] * k1[s] : 0.0;
+      lam[s] = LDS(LAM + i);
+      const bool tail = kd[s] == 2;
+      v[s][0] = tail ? wb[s] * k1[s] : 0.0;
+      v[s][1] = tail ? lam[s] * k1[s] : 0.0;
+      v[s][2] = tail ? lam[s] * k0[s] : 0.0;
     }
-    cone_reduce<1, 0>(v);
-    double y[2], y0v[2], kn[2], kn0[2];
+    cone_reduce<3, 0>(v);
+    MARK_BEGIN("tail_post1");
+    double y[2], y0v[2], kn[2], kn0[2], ly[2], lkn[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int i = 64 * s + lane, c = ci[s];
-      const double a1 = v[s][0], im = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
+      const double a1 = v[s][0];
+      const double mu = ccv(CC_MU, c), imu = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
+      const double w2 = ccv(CC_W2, c), wl = ccv(CC_WL, c);
       const double ca = LDS(CA + i);
+      const bool poc = kd[s] == 0, hd = kd[s] == 1;
       const double cy = a1 * i1 - k10[s];
-      const double y0 = im * (wb0 * k10[s] - a1);
-      y[s] = kd[s] == 0 ? ca * k1[s] : (kd[s] == 1 ? y0 : im * (k1[s] + cy * wb[s]));
-      const double a2 = im * (a1 + cy * ccv(CC_W2, c));
-      const double zs = kd[s] == 1 ? im * (wb0 * y0 - a2) : im * (y[s] + (a2 * i1 - y0) * wb[s]);
-      if (kd[s] != 3) LDS(RZ + i) = kd[s] == 0 ? ca * y[s] : zs;
+      const double y0 = imu * (wb0 * k10[s] - a1);
+      const double a2 = imu * (a1 + cy * w2);  // wbar_1'y_1
+      y[s] = poc ? ca * k1[s] : (hd ? y0 : imu * (k1[s] + cy * wb[s]));
+      const double zs = hd ? imu * (wb0 * y0 - a2) : imu * (y[s] + (a2 * i1 - y0) * wb[s]);
       y0v[s] = y0;
-      kn[s] = LDS(K0 + i) - y[s];
-      kn0[s] = LDS(K0 + eo[s]) - y0;
-      v[s][0] = kd[s] == 2 ? wb[s] * kn[s] : 0.0;
-    }
-    cone_reduce<1, 0>(v);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int i = 64 * s + lane, c = ci[s];
-      const double del = v[s][0], mu = ccv(CC_MU, c), wb0 = ccv(CC_WB0, c);
-      const double cs = kd[s] == 0 ? wb[s] * kn[s]
-                                   : (kd[s] == 1 ? mu * (wb0 * kn0[s] + del)
-                                                 : mu * (kn[s] + (kn0[s] + del * ccv(CC_I1, c)) * wb[s]));
-      if (kd[s] != 3) LDS(RS + i) = cs;
+      kn[s] = k0[s] - y[s];
+      kn0[s] = k00[s] - y0;
+      const double del = ccv(CC_DLT, c) - a2;  // wbar_1'kn_1
+      const double cs = poc ? wb[s] * kn[s]
+                            : (hd ? mu * (wb0 * kn0[s] + del) : mu * (kn[s] + (kn0[s] + del * i1) * wb[s]));
+      ly[s] = imu * (v[s][1] + cy * wl);  // lambda_1'y_1
+      lkn[s] = v[s][2] - ly[s];           // lambda_1'kn_1
+      if (kd[s] != 3) {
+        LDS(RZ + i) = poc ? ca * y[s] : zs;
+        LDS(RS + i) = cs;
+      }
     }
     if (!do_step) {
       SYNC();
       return 0.0;
     }
-    // scmax (mats.jl:42-86) of kt3 = y and kt2 = kn
-    double w[2][4], lam[2];
+    // scmax (mats.jl:42-86) of kt3 = y and kt2 = kn, and kt2'kt3
+    double w[2][5], r1y[2], r1k[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int i = 64 * s + lane;
+      const int i = 64 * s + lane, c = ci[s];
       if (kd[s] != 3) {
         LDS(T1 + i) = y[s];
         LDS(K0 + i) = kn[s];
       }
-      lam[s] = LDS(LAM + i);
-      const bool tail = kd[s] == 2, poc = kd[s] == 0;
-      w[s][0] = tail ? lam[s] * y[s] : 0.0;
-      w[s][1] = tail ? lam[s] * kn[s] : 0.0;
-      w[s][2] = poc ? -y[s] / lam[s] : -INFINITY;
-      w[s][3] = poc ? -kn[s] / lam[s] : -INFINITY;
-    }
-    cone_reduce<4, 0xC>(w);
-    double q[2][2], r1y[2], r1k[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = ci[s];
+      const bool tail = kd[s] == 2, poc = kd[s] == 0, real = kd[s] != 3;
       const double sa = ccv(CC_SA, c), l0 = ccv(CC_L0, c), sal = ccv(CC_SAL, c);
-      r1y[s] = sa * l0 * y0v[s] - sa * w[s][0];
-      r1k[s] = sa * l0 * kn0[s] - sa * w[s][1];
+      r1y[s] = sa * l0 * y0v[s] - sa * ly[s];
+      r1k[s] = sa * l0 * kn0[s] - sa * lkn[s];
       const double cyy = (r1y[s] + y0v[s]) * sal, cyk = (r1k[s] + kn0[s]) * sal;
       const double qy = sa * (y[s] - cyy * sa * lam[s]), qk = sa * (kn[s] - cyk * sa * lam[s]);
-      q[s][0] = kd[s] == 2 ? qy * qy : 0.0;
-      q[s][1] = kd[s] == 2 ? qk * qk : 0.0;
+      const double il = LDS(IL + i);
+      w[s][0] = tail ? qy * qy : 0.0;
+      w[s][1] = tail ? qk * qk : 0.0;
+      w[s][2] = poc ? -y[s] * il : -INFINITY;
+      w[s][3] = poc ? -kn[s] * il : -INFINITY;
+      w[s][4] = real ? y[s] * kn[s] : 0.0;
     }
-    cone_reduce<2, 0>(q);
+    cone_reduce<5, 0xC>(w);
+    MARK_BEGIN("tail_post2");
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = ci[s];
       if (64 * s >= k || kd[s] == 3 || 64 * s + lane != eo[s]) continue;
       const double sa = ccv(CC_SA, c);
-      const double vy = sqrt(q[s][0]) - sa * r1y[s], vk = sqrt(q[s][1]) - sa * r1k[s];
+      const double vy = sqrt(w[s][0]) - sa * r1y[s];
+      const double vk = sqrt(w[s][1]) - sa * r1k[s];
       LDS(O_TOTC + c) = kd[s] == 0 ? fmax(w[s][2], w[s][3]) : fmax(vy, vk);
+      LDS(cc(CC_KK, c)) = w[s][4];
     }
     SYNC();
     dom = dm_aa ? 1 : 0;
@@ -882,39 +973,29 @@ struct Small {
 
   // rho, sigma, mu (solver.jl:132-134) and the corrector right-hand side
   // (:136-140): kt1 = kt2 o kt3, ds += sigma mu e - kt1, dx, dy, dz *= 1 - sigma.
-  // In: K0 (kt2), T1 (kt3), DS, DZ, RD, RP.
+  // kt2'kt3 and the SOC heads of kt2 o kt3 come from solve_tail's reduction.
+  // In: K0 (kt2), T1 (kt3), KK, DS, DZ, RD, RP.
   __device__ __forceinline__ void affine_post(double tstep, double ll) {
+    MARK_BEGIN("affine_post");
     LANE_IDS();
-    double v[2][1], a2[2], a3[2], a20[2], a30[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int i = 64 * s + lane;
-      a2[s] = LDS(K0 + i);
-      a3[s] = LDS(T1 + i);
-      a20[s] = LDS(K0 + eo[s]);
-      a30[s] = LDS(T1 + eo[s]);
-      v[s][0] = kd[s] != 3 ? a2[s] * a3[s] : 0.0;
-    }
-    cone_reduce<1, 0>(v);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-      if (64 * s < k && kd[s] != 3 && 64 * s + lane == eo[s]) LDS(O_TOTC + ci[s]) = v[s][0];
-    SYNC();
     double kk = 0.0;
-    for (int c = 0; c < nc; ++c) kk += LDS(O_TOTC + c);
+    for (int c = 0; c < nc; ++c) kk += LDS(cc(CC_KK, c));
     const double t = tstep;
     const double rho = 1.0 - t - t * t * kk / ll;
     const double cr = isnan(rho) ? rho : (rho < 0.0 ? 0.0 : (rho > 1.0 ? 1.0 : rho));
     const double sig = ipow(cr, a.sigma_exp);  // max(0,min(1,rho))^3 (solver.jl:133)
     const double mu_ipm = ll / a.deg;
     const double scf = 1.0 - sig;
+    const double smu = sig * mu_ipm;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int i = 64 * s + lane;
       if (kd[s] == 3) continue;
-      const double kt1 = kd[s] == 0 ? a2[s] * a3[s] : (kd[s] == 1 ? v[s][0] : a20[s] * a3[s] + a30[s] * a2[s]);
+      const double a2 = LDS(K0 + i), a3 = LDS(T1 + i);
+      const double a20 = LDS(K0 + eo[s]), a30 = LDS(T1 + eo[s]);
+      const double kt1 = kd[s] == 0 ? a2 * a3 : (kd[s] == 1 ? LDS(cc(CC_KK, ci[s])) : a20 * a3 + a30 * a2);
       const double e = kd[s] == 2 ? 0.0 : 1.0;
-      LDS(DS + i) = LDS(DS + i) + (sig * mu_ipm * e - kt1);
+      LDS(DS + i) = LDS(DS + i) + (smu * e - kt1);
       LDS(DZ + i) = LDS(DZ + i) * scf;
     }
     for (int j = lane; j < n; j += 64) LDS(RD + j) = LDS(RD + j) * scf;
@@ -924,6 +1005,7 @@ struct Small {
 
   // max_step(-iz), max_step(iz) (mats.jl:1-28) for the initial shift (solver.jl:88-101)
   __device__ __forceinline__ void maxstep_op(int xv, double& alphp, double& alphd) {
+    MARK_BEGIN("maxstep_op");
     LANE_IDS();
     double v[2][3], x[2], x0[2];
 #pragma unroll
@@ -951,6 +1033,7 @@ struct Small {
 
   // U[c,:] = (sum_{i in cone c} w_i G[i,:]) / (1+wb0), w_head = -(1+wb0), w_tail = wb_i
   __device__ __forceinline__ void compute_U() {
+    MARK_BEGIN("compute_U");
     LANE_IDS();
     for (int c = 0; c < nc; ++c) {
       if (uni((int)LDS(O_CKIND + c)) != SOC_K) continue;
@@ -984,6 +1067,7 @@ struct Small {
 
   // ----------------------------------------------------- H = X'X (+A'A)
   __device__ __forceinline__ void form_H(bool addAA) {
+    MARK_BEGIN("form_H");
     LANE_IDS();
 #pragma unroll
     for (int t = 0; t < NT; ++t) T[t] = (d4){0.0, 0.0, 0.0, 0.0};
@@ -1185,6 +1269,7 @@ struct Small {
     }
   }
   __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok) const {
+    MARK_BEGIN("factor_tile");
     LANE_IDS();
     d4 It;
 #pragma unroll
@@ -1205,6 +1290,7 @@ struct Small {
 
   template <int Q, bool SUBST, int P = 0>
   __device__ __forceinline__ void sweep_tiles(d4 (&M)[Q * (Q + 1) / 2], const d4& Id, bool& ok) {
+    MARK_BEGIN("sweep_tiles");
     if constexpr (P < Q) {
       d4 X[Q];  // M_Pi in C/D layout (stored transposed below the pivot tile)
 #pragma unroll
@@ -1251,6 +1337,7 @@ struct Small {
   }
 
   __device__ __forceinline__ d4 transpose(d4 t) {
+    MARK_BEGIN("transpose");
     LANE_IDS();
     SYNC();
 #pragma unroll
@@ -1279,6 +1366,7 @@ struct Small {
 
   // H (+A'A) -> sweep -> Li;  ALi' = Li A' (n x m);  S = A ALi';  S^-1.
   __device__ __forceinline__ int factor(bool identity, bool addAA) {
+    MARK_BEGIN("factor");
     LANE_IDS();
     STAMP(SP_OTHER);
     if (!identity) compute_U();
@@ -1382,6 +1470,7 @@ struct Small {
   // part (transposed off-diagonal tiles): reduce over the 4 row groups.
   template <int Q>
   __device__ __forceinline__ void symv(const d4 (&M)[Q * (Q + 1) / 2], int vin, int vout) {
+    MARK_BEGIN("symv");
     LANE_IDS();
     double vc[Q], P2[Q];
 #pragma unroll
@@ -1462,6 +1551,7 @@ struct Small {
     }
   }
   __device__ __forceinline__ void gemv_G(int u, int add1, int add2, int out) {
+    MARK_BEGIN("gemv_G");
     LANE_IDS();
     double uq[NQ];
 #pragma unroll
@@ -1472,6 +1562,7 @@ struct Small {
 
   // acc[q] (all lanes) = (G' v)[16q+cl]
   __device__ __forceinline__ void gemv_Gt(int v, double (&acc)[NQ]) {
+    MARK_BEGIN("gemv_Gt");
     LANE_IDS();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
@@ -1489,6 +1580,7 @@ struct Small {
 
   // acc[q] (all lanes) = (A' v)[16q+cl]: rows split over the 4 lane groups
   __device__ __forceinline__ void At_mv(int v, double (&acc)[NQ]) {
+    MARK_BEGIN("At_mv");
     LANE_IDS();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
@@ -1507,6 +1599,7 @@ struct Small {
   // out[i] = (A u)[i] - sub[i] for i < m (columns split over the 4 lane groups);
   // returns sum of out[i]^2 on lanes g == 0
   __device__ __forceinline__ double A_mv(int u, int sub, int out) {
+    MARK_BEGIN("A_mv");
     LANE_IDS();
     double sq = 0.0;
 #pragma unroll
@@ -1527,6 +1620,7 @@ struct Small {
 
   // rd = A'y + G'z + c, rp = Ax - b, rz = Gx + s - h (solver.jl:109-118)
   __device__ __forceinline__ void residuals(double& nd, double& np_, double& gap) {
+    MARK_BEGIN("residuals");
     LANE_IDS();
     double acc[NQ], at[NQ];
     gemv_Gt(Z_, acc);
@@ -1556,6 +1650,7 @@ struct Small {
   // A*(Li*n0) - dy; cy = S^-1 m0; m0 = sing ? dy - cy : -cy (init: -cy);
   // n0 += A'm0; cx = Li n0; k1 = G cx - k2.   In: RD RP T2(=W^-2 k2) K2.  Out: RX RY K1.
   __device__ __forceinline__ void solve_matrix_part(bool init) {
+    MARK_BEGIN("solve_matrix_part");
     LANE_IDS();
     {
       double acc[NQ], at[NQ];
@@ -1640,6 +1735,7 @@ struct Small {
       int next = phase;
       switch (phase) {
         case MP_SINGTEST:  // Problem's `sing` (Socp.jl:49-56): is G'G positive definite?
+          MARK_BEGIN("case MP_SINGTEST");
           scaling_identity();
           fac_ident = true;
           fac_aa = false;
@@ -1647,10 +1743,12 @@ struct Small {
           next = MP_FACTOR;
           break;
         case MP_SINGTEST_POST:
+          MARK_BEGIN("case MP_SINGTEST_POST");
           sing = (fst == ST_CHOL_H);
           next = after_singtest;
           break;
         case MP_FACTOR:  // setup_iter (densesolver.jl:41-52)
+          MARK_BEGIN("case MP_FACTOR");
           fst = factor(fac_ident, fac_aa);
           if (fst && fret != MP_SINGTEST_POST) {
             status = fst;
@@ -1659,6 +1757,7 @@ struct Small {
           next = fret;
           break;
         case MP_INIT:  // initial point: the KKT system with W = I (solver.jl:68-84)
+          MARK_BEGIN("case MP_INIT");
           scaling_identity();
           for (int j = lane; j < n; j += 64) LDS(RD + j) = -LDS(C_ + j);
           for (int i = lane; i < m; i += 64) LDS(RP + i) = LDS(B_ + i);
@@ -1674,6 +1773,7 @@ struct Small {
           next = MP_FACTOR;
           break;
         case MP_ITER: {  // residuals (solver.jl:109-118), compute_scaling (:106), exit test (:122)
+          MARK_BEGIN("case MP_ITER");
           STAMP(SP_OTHER);
           residuals(nd, np_, gap);
           STAMP(SP_RESID);
@@ -1708,6 +1808,7 @@ struct Small {
           break;
         }
         case MP_KKT: {
+          MARK_BEGIN("case MP_KKT");
           const bool dm = scaling_op(ll, dm_aa, false);
           if (dm) {
             status = ST_DOMAIN;
@@ -1722,17 +1823,20 @@ struct Small {
           break;
         }
         case MP_SOLVE_HEAD:
+          MARK_BEGIN("case MP_SOLVE_HEAD");
           STAMP(SP_OTHER);
           solve_head();
           STAMP(SP_VOP);
           next = MP_SOLVE_MAT;
           break;
         case MP_SOLVE_MAT:
+          MARK_BEGIN("case MP_SOLVE_MAT");
           solve_matrix_part(ret == RET_INIT);
           STAMP(SP_SOLVE);
           next = MP_SOLVE_TAIL;
           break;
         case MP_SOLVE_TAIL: {
+          MARK_BEGIN("case MP_SOLVE_TAIL");
           const bool do_step = ret == RET_AFFINE || ret == RET_COMBINED;
           int dom = 0;
           const double tstep = solve_tail(do_step, dm_aa, dom);
