@@ -410,6 +410,14 @@ struct Small {
   AD G[NP][NQ];  // AGPR-resident
   d4 T[NT];
   d4 Sv[MT];
+#ifndef SOCP_KEEP_AL
+#define SOCP_KEEP_AL 0
+#endif
+  // A Li (m x n) as C/D tiles AL[tq][ti] = (A Li)[16tq.., 16ti..]: kept from
+  // the Schur step for the solves' cx = Li n0 + (A Li)' m0 (shapes with at
+  // most 4 such tiles; larger ones take A'm0 and a second Li product)
+  static constexpr bool KEEP_AL = SOCP_KEEP_AL && NQ * MQ <= 4;
+  d4 AL[KEEP_AL ? MQ : 1][KEEP_AL ? NQ : 1];
 
   __device__ __forceinline__ Small(const SmallArgs& args)
       : a(args), lane(threadIdx.x), g(threadIdx.x >> 4), cl(threadIdx.x & 15),
@@ -1066,26 +1074,61 @@ struct Small {
   }
 
   // ----------------------------------------------------- H = X'X (+A'A)
+#ifndef SOCP_SYRK_PIPE
+#define SOCP_SYRK_PIPE 1
+#endif
+  // row step pp of X = W^-1 G: X[i,:] = CA_i G[i,:] + CBV_i U[cone(i),:]
+  __device__ __forceinline__ void genX(int pp, double (&X)[NQ]) {
+    LANE_IDS();
+    const int row = 4 * pp + g;
+    const double cav = LDS(CA + row), cbv = LDS(CBV + row);
+    const int cid = ((int)LDS(O_RC + row)) >> 2;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) X[q] = fma(cav, a_get(G[pp][q]), cbv * LDS(O_U + cid * NPAD + 16 * q + cl));
+  }
   __device__ __forceinline__ void form_H(bool addAA) {
     MARK_BEGIN("form_H");
     LANE_IDS();
 #pragma unroll
     for (int t = 0; t < NT; ++t) T[t] = (d4){0.0, 0.0, 0.0, 0.0};
+#if SOCP_SYRK_PIPE
+    // software-pipelined: row step pp+1 of X is generated (LDS coefficient
+    // reads, AGPR reads of G, FMAs) while the MFMAs of step pp run, one MFMA
+    // between every few of those instructions
+    double Xc[NQ];
+    genX(0, Xc);
 #pragma unroll
     for (int pp = 0; pp < NP; ++pp) {
-      const int row = 4 * pp + g;
-      const double cav = LDS(CA + row), cbv = LDS(CBV + row);
-      const int cid = ((int)LDS(O_RC + row)) >> 2;
-      double X[NQ];
+      double Xn[NQ];
+      if (pp + 1 < NP) genX(pp + 1, Xn);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q)
-        X[q] = fma(cav, a_get(G[pp][q]), cbv * LDS(O_U + cid * NPAD + 16 * q + cl));
+      for (int ti = 0; ti < NQ; ++ti)
+#pragma unroll
+        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = mfma(Xc[ti], Xc[tj], T[tri(ti, tj)]);
+      if (pp + 1 < NP) {
+#pragma unroll
+        for (int r = 0; r < NT; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one LDS read
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // three VALU
+        }
+      }
+      SCHED_FENCE();
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) Xc[q] = Xn[q];
+    }
+#else
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp) {
+      double X[NQ];
+      genX(pp, X);
 #pragma unroll
       for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
         for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = mfma(X[ti], X[tj], T[tri(ti, tj)]);
       if (pp % 2 == 1) SCHED_FENCE();
     }
+#endif
     if (addAA) {
 #pragma unroll
       for (int tm = 0; tm < MQ; ++tm)
@@ -1207,8 +1250,12 @@ struct Small {
   // The 4x4 diagonal block is factored in wave-uniform values (its upper
   // triangle, as potrf('U') reads it), then every lane forms the block's rows
   // of R = L' and of W by forward substitution from the broadcast block rows.
-  template <int B>
-  __device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok) const {
+  struct NoHook {
+    template <int B>
+    __device__ __forceinline__ void run() const {}
+  };
+  template <int B, class H = NoHook>
+  __device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok, const H& hook = H()) const {
     if constexpr (B < 4) {
       LANE_IDS();
       double R, Wb;
@@ -1255,6 +1302,7 @@ struct Small {
         Wb = g == 0 ? W0 : (g == 1 ? W1 : (g == 2 ? W2 : W3));
       }
 #endif
+      hook.template run<B>();  // independent MFMA work interleaved with the chain
       W[B] = Wb;
       if constexpr (B < 3) {
         const d4 t = __builtin_amdgcn_mfma_f64_16x16x4f64(R, R, Dt, 0, 0, 1);   // Dt -= R'R
@@ -1265,17 +1313,18 @@ struct Small {
           It[r] = u[r];
         }
       }
-      tile_block<B + 1>(Dt, It, W, ok);
+      tile_block<B + 1>(Dt, It, W, ok, hook);
     }
   }
-  __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok) const {
+  template <class H = NoHook>
+  __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok, const H& hook = H()) const {
     MARK_BEGIN("factor_tile");
     LANE_IDS();
     d4 It;
 #pragma unroll
     for (int r = 0; r < 4; ++r) It[r] = (g + 4 * r == cl) ? 1.0 : 0.0;
     W = It;
-    tile_block<0>(Dt, It, W, ok);
+    tile_block<0>(Dt, It, W, ok, hook);
   }
 
   // tile transpose: by MFMA against the identity (X' I), no LDS hand-off, or
@@ -1288,17 +1337,79 @@ struct Small {
 #endif
   }
 
-  template <int Q, bool SUBST, int P = 0>
-  __device__ __forceinline__ void sweep_tiles(d4 (&M)[Q * (Q + 1) / 2], const d4& Id, bool& ok) {
+#ifndef SOCP_SWEEP_LOOKAHEAD
+#define SOCP_SWEEP_LOOKAHEAD 1
+#endif
+  // The MFMA work of panel P that the next pivot tile's factorisation does not
+  // wait for: the Gram updates other than tile (P+1, P+1), the new panel tiles
+  // M_Pi and M_PP.  Enumerated at compile time so it can be dealt out between
+  // the row blocks of the next factorisation (look-ahead).
+  struct PanelOp {
+    int kind, i, j;  // 0: M_ij -= Y_i'Y_j, 1: new panel tile i, 2: M_PP = -W'W, -1: none
+  };
+  template <int Q, int P>
+  static constexpr PanelOp panel_op(int idx) {
+    int cnt = 0;
+    for (int i = 0; i < Q; ++i)
+      for (int j = 0; j <= i; ++j) {
+        if (i == P || j == P || (i == P + 1 && j == P + 1)) continue;
+        if (cnt++ == idx) return PanelOp{0, i, j};
+      }
+    for (int i = 0; i < Q; ++i) {
+      if (i == P) continue;
+      if (cnt++ == idx) return PanelOp{1, i, 0};
+    }
+    if (cnt++ == idx) return PanelOp{2, P, P};
+    return PanelOp{-1, 0, 0};
+  }
+  template <int Q, int P>
+  static constexpr int panel_op_count() {
+    int c = 0;
+    while (panel_op<Q, P>(c).kind >= 0) ++c;
+    return c;
+  }
+  template <int Q, int P, int OP>
+  __device__ __forceinline__ static void do_panel_op(d4 (&M)[Q * (Q + 1) / 2], const d4 (&Y)[Q], const d4& W) {
+    constexpr PanelOp o = panel_op<Q, P>(OP);
+    const d4 z = (d4){0.0, 0.0, 0.0, 0.0};
+    if constexpr (o.kind == 0) {
+      M[tri(o.i, o.j)] = mm<1>(Y[o.i], Y[o.j], M[tri(o.i, o.j)]);  // -= Y_i'Y_j
+    } else if constexpr (o.kind == 1) {
+      if constexpr (o.i < P) M[tri(P, o.i)] = mm<0>(W, Y[o.i], z);  // W'Y_i = D^-1 M_Pi
+      else M[tri(o.i, P)] = mm<0>(Y[o.i], W, z);                    // its transpose
+    } else if constexpr (o.kind == 2) {
+      M[tri(P, P)] = mm<1>(W, W, z);  // -W'W = -D^-1
+    }
+  }
+  template <int Q, int P, int LO, int HI>
+  __device__ __forceinline__ static void do_panel_ops(d4 (&M)[Q * (Q + 1) / 2], const d4 (&Y)[Q], const d4& W) {
+    if constexpr (LO < HI) {
+      do_panel_op<Q, P, LO>(M, Y, W);
+      do_panel_ops<Q, P, LO + 1, HI>(M, Y, W);
+    }
+  }
+  // hook for the next factorisation: after row block B, a quarter of the ops
+  template <int Q, int P>
+  struct PanelHook {
+    d4 (&M)[Q * (Q + 1) / 2];
+    const d4 (&Y)[Q];
+    const d4& W;
+    template <int B>
+    __device__ __forceinline__ void run() const {
+      constexpr int N = panel_op_count<Q, P>();
+      do_panel_ops<Q, P, (N * B) / 4, (N * (B + 1)) / 4>(M, Y, W);
+    }
+  };
+
+  // Panel P of the sweep, given W = L^-1 of its pivot tile (factored by the
+  // previous panel, overlapped with that panel's MFMA work).
+  template <int Q, bool SUBST, int P>
+  __device__ __forceinline__ void sweep_panel(d4 (&M)[Q * (Q + 1) / 2], const d4& Id, const d4& W, bool& ok) {
     MARK_BEGIN("sweep_tiles");
     if constexpr (P < Q) {
       d4 X[Q];  // M_Pi in C/D layout (stored transposed below the pivot tile)
 #pragma unroll
       for (int i = P + 1; i < Q; ++i) X[i] = ttrans(M[tri(i, P)], Id);
-      STAMP_SUB(0);
-      d4 W;
-      factor_tile(M[tri(P, P)], W, ok);
-      STAMP_SUB(1);
       const d4 WT = ttrans(W, Id);
       const d4 z = (d4){0.0, 0.0, 0.0, 0.0};
       d4 Y[Q];
@@ -1306,21 +1417,31 @@ struct Small {
       for (int i = 0; i < Q; ++i)
         if (i != P) Y[i] = mm<0>(WT, i < P ? M[tri(P, i)] : X[i], z);  // W M_Pi
       STAMP_SUB(2);
-#pragma unroll
-      for (int i = 0; i < Q; ++i)
-#pragma unroll
-        for (int j = 0; j <= i; ++j)
-          if (i != P && j != P) M[tri(i, j)] = mm<1>(Y[i], Y[j], M[tri(i, j)]);  // -= Y_i'Y_j
-      STAMP_SUB(3);
-#pragma unroll
-      for (int i = 0; i < Q; ++i) {
-        if (i < P) M[tri(P, i)] = mm<0>(W, Y[i], z);  // W'Y_i = D^-1 M_Pi
-        if (i > P) M[tri(i, P)] = mm<0>(Y[i], W, z);  // its transpose
+      if constexpr (P + 1 < Q) {
+        // the next pivot tile first, then its factorisation with the rest of
+        // this panel's MFMA work dealt out between its row blocks
+        M[tri(P + 1, P + 1)] = mm<1>(Y[P + 1], Y[P + 1], M[tri(P + 1, P + 1)]);
+        d4 Wn;
+#if SOCP_SWEEP_LOOKAHEAD
+        factor_tile(M[tri(P + 1, P + 1)], Wn, ok, PanelHook<Q, P>{M, Y, W});
+#else
+        do_panel_ops<Q, P, 0, panel_op_count<Q, P>()>(M, Y, W);
+        factor_tile(M[tri(P + 1, P + 1)], Wn, ok);
+#endif
+        STAMP_SUB(1);
+        sweep_panel<Q, SUBST, P + 1>(M, Id, Wn, ok);
+      } else {
+        do_panel_ops<Q, P, 0, panel_op_count<Q, P>()>(M, Y, W);
+        STAMP_SUB(3);
       }
-      M[tri(P, P)] = mm<1>(W, W, z);  // -W'W = -D^-1
-      STAMP_SUB(4);
-      sweep_tiles<Q, SUBST, P + 1>(M, Id, ok);
     }
+  }
+  template <int Q, bool SUBST>
+  __device__ __forceinline__ void sweep_tiles(d4 (&M)[Q * (Q + 1) / 2], const d4& Id, bool& ok) {
+    d4 W;
+    factor_tile(M[tri(0, 0)], W, ok);
+    STAMP_SUB(0);
+    sweep_panel<Q, SUBST, 0>(M, Id, W, ok);
   }
 
   // Symmetric sweep of every pivot of M (lower tiles; padding rows carry an
@@ -1433,6 +1554,10 @@ struct Small {
 #pragma unroll
           for (int s = 0; s < 4; ++s) acc = mfma(LDS(O_A + (16 * tm + cl) * LDA + 16 * tk + g + 4 * s), ALc[tk][s], acc);
         Sv[tri(tm, tq)] = acc;
+      }
+      if constexpr (KEEP_AL) {
+#pragma unroll
+        for (int ti = 0; ti < NQ; ++ti) AL[tq][ti] = transpose(ALc[ti]);  // A Li = (Li A')'
       }
     }
 #pragma unroll
@@ -1673,17 +1798,42 @@ struct Small {
     symv<MQ>(Sv, M0, RY);  // cy = S^-1 m0
     if (lane < m) LDS(M0 + lane) = (sing && !init) ? LDS(RP + lane) - LDS(RY + lane) : -LDS(RY + lane);
     SYNC();
-    {
+    if constexpr (KEEP_AL) {
+      // cx = Li (n0 + A'm0) = Li n0 + (A Li)' m0
+      ALt_mv(M0, TN, RX);
+    } else {
       double at[NQ];
       At_mv(M0, at);
       if (g == 0) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) LDS(N0 + 16 * q + cl) = LDS(N0 + 16 * q + cl) + at[q];
       }
+      SYNC();
+      symv<NQ>(T, N0, RX);  // cx = Li n0
+    }
+    gemv_G(RX, -1, K2, K1);
+  }
+
+  // out[j] = add[j] + ((A Li)' v)[j]: per tile column, an in-lane sum over the
+  // tile's rows (registers) and the four row groups (rows_sum)
+  __device__ __forceinline__ void ALt_mv(int v, int add, int out) {
+    LANE_IDS();
+    double vr[MQ][4];
+#pragma unroll
+    for (int tq = 0; tq < MQ; ++tq)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) vr[tq][r] = LDS(v + 16 * tq + g + 4 * r);
+#pragma unroll
+    for (int ti = 0; ti < NQ; ++ti) {
+      double acc = 0.0;
+#pragma unroll
+      for (int tq = 0; tq < MQ; ++tq)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = fma(AL[KEEP_AL ? tq : 0][KEEP_AL ? ti : 0][r], vr[tq][r], acc);
+      acc = rows_sum(acc);
+      if (g == 0) LDS(out + 16 * ti + cl) = acc + LDS(add + 16 * ti + cl);
     }
     SYNC();
-    symv<NQ>(T, N0, RX);   // cx = Li n0
-    gemv_G(RX, -1, K2, K1);
   }
 
   // ------------------------------------------------------------- driver
