@@ -164,6 +164,46 @@ int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims,
                          double* cx, double* cy, double* cz, double* cs,
                          int32_t* kkt_status, int32_t flags);  /* flags: SOCP_F_DEVICE_PTRS | SOCP_F_FORCE_LARGE */
 
+/* The same two methods split the way the reference's KKTSolver plugin is
+ * (densesolver.jl): a handle stands for a batch of DenseSolver objects.
+ *   socp_dense_create      replaces DenseSolver(...) construction
+ *                          (densesolver.jl:9-39): A and G (and sing, or NULL
+ *                          for the cholesky(G'G) test at every setup) are
+ *                          copied into the handle once;
+ *   socp_dense_setup_iter  replaces setup_iter(ss, pr, state, scaling)
+ *                          (densesolver.jl:41-52): NT scaling of (s, z), H,
+ *                          H^-1, A H^-1 A' and its inverse, kept on the device
+ *                          as one factor record per problem;
+ *                          status[p]: 0, SOCP_CHOL_H_FAILED,
+ *                          SOCP_CHOL_S_FAILED or SOCP_DOMAIN_ERROR (where the
+ *                          reference throws PosDefException / DomainError);
+ *   socp_dense_solve_kkt   replaces solve_kkt(ss, ...) (densesolver.jl:54-90)
+ *                          against the last setup_iter; call it any number of
+ *                          times (the solver calls it twice per iteration,
+ *                          solver.jl:125-145).  status[p] = 0, or setup_iter's
+ *                          status with NaN outputs for a problem whose setup
+ *                          failed.
+ * flags (at create, for all calls of the handle): SOCP_F_DEVICE_PTRS (every
+ * pointer, A and G included, is a device pointer; the calls are then
+ * stream-ordered on the context's stream and return without synchronising) |
+ * SOCP_F_FORCE_LARGE.  With host pointers each setup_iter moves 2k doubles
+ * per problem host-to-device and each solve_kkt n+m+2k; A and G move once, at
+ * create (socp_dense_h2d_bytes reports the last call's count).  The results are
+ * bitwise those of socp_batch_kkt_solve on the same inputs.  Device memory:
+ * socp_dense_record_bytes() per problem plus A, G. */
+typedef struct socp_dense socp_dense;
+int socp_dense_create(socp_ctx* ctx, const socp_dims* dims,
+                      const int32_t* cone_kind, const int32_t* cone_offs, const int32_t* cone_dim,
+                      const double* A, const double* G, const uint8_t* sing, int32_t flags,
+                      socp_dense** out);
+int socp_dense_setup_iter(socp_dense* h, const double* s, const double* z, int32_t* status);
+int socp_dense_solve_kkt(socp_dense* h, const double* dx, const double* dy, const double* dz,
+                         const double* ds, double* cx, double* cy, double* cz, double* cs,
+                         int32_t* status);
+int socp_dense_h2d_bytes(const socp_dense* h, int64_t* bytes);
+int64_t socp_dense_record_bytes(const socp_dense* h);
+int socp_dense_destroy(socp_dense* h);
+
 /* Device-side deterministic generator of feasible synthetic problems
  * (SURVEY.md §8(d)): counter-based SplitMix64 keyed on the GLOBAL problem
  * index first_problem + p, so shards of a multi-GPU run reproduce the same

@@ -243,10 +243,12 @@ static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_D
 static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
   size_t lds = small_lds_bytes(v->NQ, v->NP, v->MQ);
   if (lds > 160 * 1024) return fail(SOCP_E_UNSUPPORTED, "LDS footprint too large");
+  const bool solver = args.mode == MODE_SOLVE;
+  const void* kern = solver ? v->kernel : v->kkt_kernel;
   if (lds > 64 * 1024)
-    HIPCHK(hipFuncSetAttribute(v->kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v->kernel, 64, lds));
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds));
   if (per_cu < 1) per_cu = 1;
   int64_t blocks = (int64_t)ctx->num_cu * per_cu;
   if (blocks > args.B) blocks = args.B;
@@ -255,13 +257,13 @@ static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
   args.stamps = g_stamps;
   void* kargs[] = {&args};
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
-  HIPCHK(hipLaunchKernel(v->kernel, dim3((unsigned)blocks), dim3(64), kargs, lds, ctx->stream));
+  HIPCHK(hipLaunchKernel(kern, dim3((unsigned)blocks), dim3(64), kargs, lds, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
-  ctx->last_name = v->name;
+  ctx->last_name = solver ? v->name : v->kkt_name;
   return 0;
 }
 
-static int launch_large(socp_ctx* ctx, const SmallArgs& a) {
+static int launch_large(socp_ctx* ctx, const SmallArgs& a, double* rec = nullptr) {
   size_t lds = 0;
   if (!large_fits(a.n, a.m, a.k, a.nc, &lds)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
   const void* kern = large_kernel_ptr();
@@ -280,6 +282,7 @@ static int launch_large(socp_ctx* ctx, const SmallArgs& a) {
   const int rc = ctx->buf[socp_ctx::B_LWS].ensure((size_t)grid * (size_t)L.w_total * sizeof(double));
   if (rc) return fail(rc, "workspace allocation failed");
   la.ws = (double*)ctx->buf[socp_ctx::B_LWS].p;
+  la.rec = rec;
   HIPCHK(hipMemsetAsync(a.counter, 0, sizeof(int32_t), ctx->stream));
   void* kargs[] = {&la};
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
@@ -557,6 +560,221 @@ extern "C" int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims, const 
   TRY(copy_back(ctx, kkt_status, a.status, (size_t)B, dev));
   if (!dev) HIPCHK(hipStreamSynchronize(ctx->stream));
   return 0;
+}
+
+// -------------------------------------------------------- dense handles
+// The reference's solver plugin split (densesolver.jl): the solver object is
+// built once per problem (A, G kept), setup_iter (:41-52) factors for the
+// current (s, z), and solve_kkt (:54-90) is called twice per iteration against
+// that factorisation.  A handle keeps A, G (and sing) resident and one factor
+// record per problem; a setup_iter call moves s, z in and a solve_kkt call one
+// right-hand side, so per-call H2D traffic is O(n + m + k) per problem.
+struct socp_dense {
+  socp_ctx* ctx = nullptr;
+  SmallArgs a;  // problem part filled at create
+  const SmallVariant* v = nullptr;
+  int64_t rec_stride = 0;
+  bool ready = false;      // setup_iter has run
+  int64_t h2d_bytes = 0;   // host-to-device bytes moved by the last call
+  enum { D_A, D_G, D_SING, D_ZERO, D_REC, D_S, D_Z, D_DX, D_DY, D_DZ, D_DS, D_CX, D_CY, D_CZ, D_CS,
+         D_ST, D_CNT, ND };
+  DevBuf buf[ND];
+};
+
+static void dense_free(socp_dense* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->ctx->device);
+  (void)hipStreamSynchronize(h->ctx->stream);
+  for (auto& b : h->buf) b.release();
+  delete h;
+}
+
+// copies `count` elements into handle buffer `slot`: from the host (counted in
+// h2d_bytes) or, with SOCP_F_DEVICE_PTRS, device to device
+template <class T>
+static int dense_in(socp_dense* h, int slot, const T* src, size_t count, bool dev, const T** out) {
+  if (!src || count == 0) {
+    *out = src;
+    return 0;
+  }
+  if (dev) {
+    *out = src;
+    return 0;
+  }
+  int rc = h->buf[slot].ensure(count * sizeof(T));
+  if (rc) return fail(rc, "device allocation failed");
+  HIPCHK(hipMemcpyAsync(h->buf[slot].p, src, count * sizeof(T), hipMemcpyHostToDevice, h->ctx->stream));
+  h->h2d_bytes += (int64_t)(count * sizeof(T));
+  *out = (const T*)h->buf[slot].p;
+  return 0;
+}
+template <class T>
+static int dense_out(socp_dense* h, int slot, T* user, size_t count, bool dev, T** out) {
+  if (!user || count == 0 || dev) {
+    *out = user;
+    return 0;
+  }
+  int rc = h->buf[slot].ensure(count * sizeof(T));
+  if (rc) return fail(rc, "device allocation failed");
+  *out = (T*)h->buf[slot].p;
+  return 0;
+}
+
+extern "C" int socp_dense_create(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,
+                                 const int32_t* cone_offs, const int32_t* cone_dim, const double* A,
+                                 const double* G, const uint8_t* sing, int32_t flags, socp_dense** out) {
+  if (!out) return fail(SOCP_E_INVALID, "out is NULL");
+  *out = nullptr;
+  if (!ctx) return fail(SOCP_E_INVALID, "ctx is NULL");
+  socp_dense* h = new socp_dense();
+  h->ctx = ctx;
+  SmallArgs& a = h->a;
+  memset(&a, 0, sizeof(a));
+  int degree = 0;
+  auto bail = [&](int rc) {
+    dense_free(h);
+    return rc;
+  };
+  int rc = check_problem(dims, cone_kind, cone_offs, cone_dim, &a.cones, &degree);
+  if (rc) return bail(rc);
+  const int64_t B = dims->batch;
+  const int n = dims->n, m = dims->m, k = dims->k;
+  if (B > 0 && (!G || (m > 0 && !A))) return bail(fail(SOCP_E_INVALID, "NULL data pointer"));
+  const bool force_large = (flags & SOCP_F_FORCE_LARGE) != 0;
+  h->v = (force_large || dims->ncones > NCS) ? nullptr : pick_variant(n, m, k);
+  if (!h->v && !large_fits(n, m, k, dims->ncones, nullptr)) return bail(fail(SOCP_E_UNSUPPORTED, kUnsupported));
+  if (hipSetDevice(ctx->device) != hipSuccess) return bail(fail(SOCP_E_HIP, "hipSetDevice"));
+  const bool dev = (flags & SOCP_F_DEVICE_PTRS) != 0;
+  a.B = B;
+  a.n = n;
+  a.m = m;
+  a.k = k;
+  a.nc = dims->ncones;
+  a.deg = degree;
+  a.maxit = 1;
+  a.sigma_exp = 3;
+  a.flags = flags & SOCP_F_DEVICE_PTRS;
+  if (B == 0) {
+    *out = h;
+    return 0;
+  }
+  typedef socp_dense D;
+  // the handle owns its copies (the caller's device buffers may be reused)
+  auto own = [&](int slot, const void* src, size_t bytes) -> int {
+    if (!src || bytes == 0) return 0;
+    if (h->buf[slot].ensure(bytes)) return fail(SOCP_E_NOMEM, "device allocation failed");
+    HIPCHK(hipMemcpyAsync(h->buf[slot].p, src, bytes, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                          ctx->stream));
+    if (!dev) h->h2d_bytes += (int64_t)bytes;
+    return 0;
+  };
+  if ((rc = own(D::D_A, A, (size_t)B * m * n * sizeof(double)))) return bail(rc);
+  if ((rc = own(D::D_G, G, (size_t)B * k * n * sizeof(double)))) return bail(rc);
+  if ((rc = own(D::D_SING, sing, (size_t)B))) return bail(rc);
+  a.A = m > 0 ? (const double*)h->buf[D::D_A].p : nullptr;
+  a.G = (const double*)h->buf[D::D_G].p;
+  a.sing = sing ? (const uint8_t*)h->buf[D::D_SING].p : nullptr;
+  // c, b, h are not used by setup_iter / solve_kkt but the loader reads them
+  const size_t zb = (size_t)B * (n + m + k) * sizeof(double);
+  if (h->buf[D::D_ZERO].ensure(zb)) return bail(fail(SOCP_E_NOMEM, "device allocation failed"));
+  if (hipMemsetAsync(h->buf[D::D_ZERO].p, 0, zb, ctx->stream) != hipSuccess)
+    return bail(fail(SOCP_E_HIP, "hipMemsetAsync"));
+  a.c = (const double*)h->buf[D::D_ZERO].p;
+  a.b = a.c + (size_t)B * n;
+  a.h = a.b + (size_t)B * m;
+  h->rec_stride = h->v ? small_rec_doubles(h->v->NQ, h->v->NP, h->v->MQ) : large_layout(n, m, k).r_total;
+  if (h->buf[D::D_REC].ensure((size_t)B * (size_t)h->rec_stride * sizeof(double)))
+    return bail(fail(SOCP_E_NOMEM, "factor record allocation failed"));
+  if (h->buf[D::D_CNT].ensure(256)) return bail(fail(SOCP_E_NOMEM, "device allocation failed"));
+  a.counter = (int32_t*)h->buf[D::D_CNT].p;
+  a.rec = (double*)h->buf[D::D_REC].p;
+  a.rec_stride = h->rec_stride;
+  *out = h;
+  return 0;
+}
+
+extern "C" int socp_dense_destroy(socp_dense* h) {
+  dense_free(h);
+  return 0;
+}
+
+static int dense_launch(socp_dense* h, SmallArgs& a) {
+  return h->v ? launch_small(h->ctx, a, h->v) : launch_large(h->ctx, a, a.rec);
+}
+
+extern "C" int socp_dense_setup_iter(socp_dense* h, const double* s, const double* z, int32_t* status) {
+  if (!h) return fail(SOCP_E_INVALID, "handle is NULL");
+  h->h2d_bytes = 0;
+  SmallArgs a = h->a;
+  const int64_t B = a.B;
+  if (B == 0) {
+    h->ready = true;
+    return 0;
+  }
+  if (!s || !z || !status) return fail(SOCP_E_INVALID, "NULL data pointer");
+  socp_ctx* ctx = h->ctx;
+  HIPCHK(hipSetDevice(ctx->device));
+  const bool dev = (a.flags & SOCP_F_DEVICE_PTRS) != 0;
+  typedef socp_dense D;
+  const size_t k = (size_t)a.k;
+  const double *ds_, *dz_;
+  TRY(dense_in(h, D::D_S, s, (size_t)B * k, dev, &ds_));
+  TRY(dense_in(h, D::D_Z, z, (size_t)B * k, dev, &dz_));
+  a.s = const_cast<double*>(ds_);  // read only in MODE_SETUP
+  a.z = const_cast<double*>(dz_);
+  TRY(dense_out(h, D::D_ST, status, (size_t)B, dev, &a.status));
+  a.mode = MODE_SETUP;
+  TRY(dense_launch(h, a));
+  TRY(copy_back(ctx, status, a.status, (size_t)B, dev));
+  if (!dev) HIPCHK(hipStreamSynchronize(ctx->stream));
+  h->ready = true;
+  return 0;
+}
+
+extern "C" int socp_dense_solve_kkt(socp_dense* h, const double* dx, const double* dy, const double* dz,
+                                    const double* ds, double* cx, double* cy, double* cz, double* cs,
+                                    int32_t* status) {
+  if (!h) return fail(SOCP_E_INVALID, "handle is NULL");
+  if (!h->ready) return fail(SOCP_E_INVALID, "solve_kkt before setup_iter");
+  h->h2d_bytes = 0;
+  SmallArgs a = h->a;
+  const int64_t B = a.B;
+  if (B == 0) return 0;
+  const int n = a.n, m = a.m, k = a.k;
+  if (!dx || !dz || !ds || !cx || !cz || !cs || !status || (m > 0 && (!dy || !cy)))
+    return fail(SOCP_E_INVALID, "NULL data pointer");
+  socp_ctx* ctx = h->ctx;
+  HIPCHK(hipSetDevice(ctx->device));
+  const bool dev = (a.flags & SOCP_F_DEVICE_PTRS) != 0;
+  typedef socp_dense D;
+  TRY(dense_in(h, D::D_DX, dx, (size_t)B * n, dev, &a.dx));
+  TRY(dense_in(h, D::D_DY, dy, (size_t)B * m, dev, &a.dy));
+  TRY(dense_in(h, D::D_DZ, dz, (size_t)B * k, dev, &a.dz));
+  TRY(dense_in(h, D::D_DS, ds, (size_t)B * k, dev, &a.ds));
+  TRY(dense_out(h, D::D_CX, cx, (size_t)B * n, dev, &a.cx));
+  TRY(dense_out(h, D::D_CY, cy, (size_t)B * m, dev, &a.cy));
+  TRY(dense_out(h, D::D_CZ, cz, (size_t)B * k, dev, &a.cz));
+  TRY(dense_out(h, D::D_CS, cs, (size_t)B * k, dev, &a.cs));
+  TRY(dense_out(h, D::D_ST, status, (size_t)B, dev, &a.status));
+  a.mode = MODE_SOLVEKKT;
+  TRY(dense_launch(h, a));
+  TRY(copy_back(ctx, cx, a.cx, (size_t)B * n, dev));
+  TRY(copy_back(ctx, cy, a.cy, (size_t)B * m, dev));
+  TRY(copy_back(ctx, cz, a.cz, (size_t)B * k, dev));
+  TRY(copy_back(ctx, cs, a.cs, (size_t)B * k, dev));
+  TRY(copy_back(ctx, status, a.status, (size_t)B, dev));
+  if (!dev) HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+extern "C" int socp_dense_h2d_bytes(const socp_dense* h, int64_t* bytes) {
+  if (!h || !bytes) return fail(SOCP_E_INVALID, "NULL argument");
+  *bytes = h->h2d_bytes;
+  return 0;
+}
+
+extern "C" int64_t socp_dense_record_bytes(const socp_dense* h) {
+  return h ? h->rec_stride * (int64_t)sizeof(double) : 0;
 }
 
 // ------------------------------------------------------------- generator

@@ -9,8 +9,10 @@ namespace socp {
 
 struct SmallVariant {
   int NQ, NP, MQ;
-  const void* kernel;  // socp_small_kernel<NQ,NP,MQ>
+  const void* kernel;  // socp_small_kernel<NQ,NP,MQ,0>: MODE_SOLVE
   const char* name;
+  const void* kkt_kernel;  // socp_small_kernel<NQ,NP,MQ,1>: MODE_KKT / MODE_SETUP / MODE_SOLVEKKT
+  const char* kkt_name;
 };
 
 // table of compiled register-resident variants, ordered by (NQ, NP, MQ)
@@ -26,7 +28,9 @@ struct LargeLayout {
   // LDS offsets (doubles)
   int o_rc, o_cc, o_kv, o_nv, o_mv, o_row, o_rv, o_part, o_red, o_fx, total;
   // workspace-slot offsets (doubles)
-  int64_t w_x, w_h, w_ap, w_at, w_yp, w_rv, w_t, w_s, w_total;
+  int64_t w_x, w_h, w_ap, w_at, w_yp, w_rv, w_t, w_s, w_v, w_total;
+  // per-problem factor record (socp_dense handles): what solve_kkt reads
+  int64_t r_h, r_ap, r_at, r_t, r_s, r_v, r_total;
 };
 __host__ __device__ inline int64_t large_al(int64_t v) { return (v + 31) / 32 * 32; }
 __host__ __device__ inline LargeLayout large_layout(int n, int m, int k) {
@@ -56,13 +60,23 @@ __host__ __device__ inline LargeLayout large_layout(int n, int m, int k) {
   L.w_rv = w; w += large_al((int64_t)L.RW);             // sweep: -1/d of every pivot
   L.w_t = w;  w += large_al((int64_t)L.NPAD * L.MPAD);  // Li A'
   L.w_s = w;  w += large_al((int64_t)L.MPAD * L.MPAD);  // S -> S^-1
+  L.w_v = w;  w += large_al(3 * (int64_t)L.KP + 12 * MAXC + 8);  // LAM WB CA, CC_*, sing, status
   L.w_total = w;
+  w = 0;
+  L.r_h = w;  w += large_al((int64_t)L.NPAD * L.NPAD);
+  L.r_ap = w; w += large_al((int64_t)L.MPAD * L.NPAD);
+  L.r_at = w; w += large_al((int64_t)L.NPAD * L.MPAD);
+  L.r_t = w;  w += large_al((int64_t)L.NPAD * L.MPAD);
+  L.r_s = w;  w += large_al((int64_t)L.MPAD * L.MPAD);
+  L.r_v = w;  w += large_al(3 * (int64_t)L.KP + 12 * MAXC + 8);
+  L.r_total = w;
   return L;
 }
 struct LargeArgs {
   SmallArgs a;
   double* ws;       // grid * wstride doubles
   int64_t wstride;  // doubles per workspace slot
+  double* rec;      // MODE_SETUP / MODE_SOLVEKKT: per-problem records (B x r_total), else NULL
 };
 const void* large_kernel_ptr();
 const char* large_kernel_name();

@@ -90,7 +90,10 @@ struct Large {
   int kpoc, csoc;  // POC elements (POC cones come first) and index of the first SOC cone
   bool sing;
   gcdbl* Gp;
-  gdbl *Xw, *Hm, *Ap, *At, *Yp, *Rv, *Tm, *Sm;
+  gdbl *Xw, *Hm, *Ap, *At, *Yp, *Rv, *Tm, *Sm, *Vr;
+  gdbl* const ws0;
+  gdbl* const rec0;
+  const int64_t wstride;
   // LDS vector offsets (doubles)
   int H_, Z_, S_, DZ, DS, RZ, RS, LAM, WB, CA, K0, K1, K2, T1, T2;
   int C_, X_, RD, RX, N0, TN;
@@ -100,16 +103,9 @@ struct Large {
   __device__ Large(const LargeArgs& la)
       : a(la.a), L(large_layout(la.a.n, la.a.m, la.a.k)), n(la.a.n), m(la.a.m), k(la.a.k),
         nc(la.a.nc), tid(threadIdx.x), lane(threadIdx.x & 63),
-        wv(__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6)) {
-    gdbl* ws = (gdbl*)la.ws + (int64_t)blockIdx.x * la.wstride;
-    Xw = ws + L.w_x;
-    Hm = ws + L.w_h;
-    Ap = ws + L.w_ap;
-    At = ws + L.w_at;
-    Yp = ws + L.w_yp;
-    Rv = ws + L.w_rv;
-    Tm = ws + L.w_t;
-    Sm = ws + L.w_s;
+        wv(__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6)), ws0((gdbl*)la.ws), rec0((gdbl*)la.rec),
+        wstride(la.wstride) {
+    set_slot(blockIdx.x);
     const int kv = L.o_kv, KP = L.KP;
     H_ = kv;
     Z_ = kv + KP;
@@ -147,6 +143,57 @@ struct Large {
     }
     sing = false;
     Gp = (gcdbl*)a.G;
+  }
+
+  __device__ void set_slot(int64_t slot) {
+    gdbl* ws = ws0 + slot * wstride;
+    Xw = ws + L.w_x;
+    Hm = ws + L.w_h;
+    Ap = ws + L.w_ap;
+    At = ws + L.w_at;
+    Yp = ws + L.w_yp;
+    Rv = ws + L.w_rv;
+    Tm = ws + L.w_t;
+    Sm = ws + L.w_s;
+    Vr = ws + L.w_v;
+  }
+  // the matrices solve_kkt reads move to problem p's record
+  __device__ void set_record(int64_t p) {
+    gdbl* r = rec0 + p * L.r_total;
+    Hm = r + L.r_h;
+    Ap = r + L.r_ap;
+    At = r + L.r_at;
+    Tm = r + L.r_t;
+    Sm = r + L.r_s;
+    Vr = r + L.r_v;
+  }
+
+  // setup_iter's cone state for the later solve_kkt calls (densesolver.jl:41-52
+  // keeps it in the solver object): LAM WB CA, the per-cone constants, sing.
+  // The matrices (Li, A, Li A', S^-1) stay where factor() left them: with a
+  // record buffer (set_record) they are the problem's own; X, the pivot rows
+  // and 1/d stay in the workgroup's scratch slot.
+  __device__ void store_record() {
+    const int KP = L.KP;
+    for (int i = tid; i < KP; i += NTH) {
+      Vr[i] = LV(LAM + i);
+      Vr[KP + i] = LV(WB + i);
+      Vr[2 * KP + i] = LV(CA + i);
+    }
+    for (int i = tid; i < 12 * MAXC; i += NTH) Vr[3 * KP + i] = LV(L.o_cc + i);
+    if (tid == 0) Vr[3 * KP + 12 * MAXC] = sing ? 1.0 : 0.0;
+    BAR();
+  }
+  __device__ void load_record() {
+    const int KP = L.KP;
+    for (int i = tid; i < KP; i += NTH) {
+      LV(LAM + i) = Vr[i];
+      LV(WB + i) = Vr[KP + i];
+      LV(CA + i) = Vr[2 * KP + i];
+    }
+    for (int i = tid; i < 12 * MAXC; i += NTH) LV(L.o_cc + i) = Vr[3 * KP + i];
+    sing = __builtin_amdgcn_readfirstlane((int)Vr[3 * KP + 12 * MAXC]) != 0;
+    BAR();
   }
 
   __device__ __forceinline__ double ccv(int q, int c) const { return LV(L.o_cc + q * MAXC + c); }
@@ -1179,26 +1226,66 @@ struct Large {
   // flow and status rules.
   __device__ void run(int64_t p) {
     LSTAMP(SP_OTHER);
+    if (rec0) set_record(p);
     load(p);
     LSTAMP(SP_LOAD);
     int status = ST_MAXIT, iters = 0;
     double nd = NAN, np_ = NAN, gap = NAN, ll = 0.0;
     bool dm_aa = false;
+    if (a.mode == MODE_SOLVEKKT) {  // solve_kkt against the setup_iter record
+      const int st0 = (int)Vr[3 * L.KP + 12 * MAXC + 1];
+      if (st0) {  // setup_iter failed for this problem: NaN solution, its status
+        for (int j = tid; j < n; j += NTH) a.cx[p * n + j] = NAN;
+        for (int i = tid; i < m; i += NTH) a.cy[p * m + i] = NAN;
+        for (int i = tid; i < k; i += NTH) {
+          a.cz[p * k + i] = NAN;
+          a.cs[p * k + i] = NAN;
+        }
+        if (tid == 0) a.status[p] = st0;
+        BAR();
+        return;
+      }
+      load_record();
+      for (int i = tid; i < k; i += NTH) {
+        LV(DZ + i) = a.dz[p * k + i];
+        LV(DS + i) = a.ds[p * k + i];
+      }
+      for (int j = tid; j < n; j += NTH) LV(RD + j) = a.dx[p * n + j];
+      for (int i = tid; i < m; i += NTH) LV(RP + i) = a.dy[p * m + i];
+      BAR();
+      solve_head();
+      solve_matrix_part(false);
+      int dom = 0;
+      solve_tail(false, dm_aa, dom);
+      for (int j = tid; j < n; j += NTH) a.cx[p * n + j] = LV(RX + j);
+      for (int i = tid; i < m; i += NTH) a.cy[p * m + i] = LV(RY + i);
+      for (int i = tid; i < k; i += NTH) {
+        a.cz[p * k + i] = LV(RZ + i);
+        a.cs[p * k + i] = LV(RS + i);
+      }
+      if (tid == 0) a.status[p] = 0;
+      BAR();
+      return;
+    }
     if (a.sing) {
       sing = a.sing[p] != 0;
     } else {  // Problem's `sing` (Socp.jl:49-56): does cholesky(G'G) fail?
       scaling_identity();
       sing = factor(false, true) == ST_CHOL_H;
     }
-    if (a.mode == MODE_KKT) {
+    if (a.mode == MODE_KKT || a.mode == MODE_SETUP) {
       for (int i = tid; i < k; i += NTH) {
         LV(S_ + i) = a.s[p * k + i];
         LV(Z_ + i) = a.z[p * k + i];
-        LV(DZ + i) = a.dz[p * k + i];
-        LV(DS + i) = a.ds[p * k + i];
+        if (a.mode == MODE_KKT) {
+          LV(DZ + i) = a.dz[p * k + i];
+          LV(DS + i) = a.ds[p * k + i];
+        }
       }
-      for (int j = tid; j < n; j += NTH) LV(RD + j) = a.dx[p * n + j];
-      for (int i = tid; i < m; i += NTH) LV(RP + i) = a.dy[p * m + i];
+      if (a.mode == MODE_KKT) {
+        for (int j = tid; j < n; j += NTH) LV(RD + j) = a.dx[p * n + j];
+        for (int i = tid; i < m; i += NTH) LV(RP + i) = a.dy[p * m + i];
+      }
       BAR();
       if (scaling_op(ll, dm_aa, false)) {
         status = ST_DOMAIN;
@@ -1206,6 +1293,9 @@ struct Large {
         const int f = factor(sing, false);
         if (f) {
           status = f;
+        } else if (a.mode == MODE_SETUP) {
+          store_record();
+          status = 0;
         } else {
           solve_head();
           solve_matrix_part(false);
@@ -1220,7 +1310,10 @@ struct Large {
           }
         }
       }
-      if (tid == 0) a.status[p] = status;
+      if (tid == 0) {
+        a.status[p] = status;
+        if (a.mode == MODE_SETUP) Vr[3 * L.KP + 12 * MAXC + 1] = (double)status;
+      }
       BAR();
       return;
     }

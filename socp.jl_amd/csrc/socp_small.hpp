@@ -44,7 +44,10 @@ struct ConeTable {
   int32_t dim[MAXC];
 };
 
-enum { MODE_SOLVE = 0, MODE_KKT = 1 };
+// MODE_SETUP / MODE_SOLVEKKT: the two plugin calls of densesolver.jl
+// (setup_iter :41-52 keeps scaling + H^-1 + S^-1 in a per-problem device
+// record; solve_kkt :54-90 solves one right-hand side against it)
+enum { MODE_SOLVE = 0, MODE_KKT = 1, MODE_SETUP = 2, MODE_SOLVEKKT = 3 };
 enum { ST_CONVERGED = 0, ST_MAXIT = 1, ST_CHOL_H = 2, ST_CHOL_S = 3, ST_DOMAIN = 4 };
 enum { F_WARM = 2 };
 
@@ -65,6 +68,8 @@ struct SmallArgs {
   double* dbg;                 // optional (KKT mode): per problem H[n*n], Li[n*n], lam[k], wb[k]
   unsigned long long* stamps;  // SOCP_DIAG builds: per-phase cycle totals
   ConeTable cones;
+  double* rec;                 // MODE_SETUP / MODE_SOLVEKKT: per-problem factor records
+  int64_t rec_stride;          // doubles per record
 };
 
 // ------------------------------------------------------------ LDS layout
@@ -116,6 +121,13 @@ struct Shape {
 };
 enum : int { NV_C, NV_X, NV_RD, NV_RX, NV_N0, NV_TN };
 enum : int { MV_B, MV_Y, MV_RP, MV_RY, MV_M0, MV_TM };
+
+// doubles of one factor record of the register kernel: the H^-1 and S^-1
+// tiles in lane order, LAM WB CA CBV IL, the per-cone constants, the sing flag
+inline int64_t small_rec_doubles(int NQ, int NP, int MQ) {
+  const int64_t NT = NQ * (NQ + 1) / 2, MT = MQ * (MQ + 1) / 2;
+  return (NT + MT) * 256 + 5 * (int64_t)(4 * NP) + 20 * NCS + 8;
+}
 
 inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
   int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = NPAD + 1;
@@ -373,7 +385,7 @@ struct RSCount<C, 0> {
 // driver micro-phases and solve kinds
 enum : int {
   MP_SINGTEST, MP_SINGTEST_POST, MP_FACTOR, MP_INIT, MP_ITER, MP_KKT,
-  MP_SOLVE_HEAD, MP_SOLVE_MAT, MP_SOLVE_TAIL
+  MP_SOLVE_HEAD, MP_SOLVE_MAT, MP_SOLVE_TAIL, MP_SAVE
 };
 enum : int { RET_INIT, RET_KKT, RET_AFFINE, RET_COMBINED };
 
@@ -1836,11 +1848,68 @@ struct Small {
     SYNC();
   }
 
+  // ------------------------------------------------------- factor record
+  // setup_iter's products for the later solve_kkt calls: H^-1 and S^-1 in
+  // register-tile (lane) order, the scaling vectors and per-cone constants the
+  // solves read, and `sing` (densesolver.jl:41-52 keeps them in the solver
+  // object; here one record per problem in HBM).
+  static __device__ constexpr int rec_kv(int v) {
+    return v == 0 ? KV_LAM : v == 1 ? KV_WB : v == 2 ? KV_CA : v == 3 ? KV_CB : KV_IL;
+  }
+  static constexpr int64_t REC_SING = (int64_t)(NT + MT) * 256 + 5 * KP + 20 * NCS;
+  static constexpr int64_t REC_STATUS = REC_SING + 1;  // setup_iter's status, read first by solve_kkt
+  __device__ __forceinline__ void store_record(int64_t p) {
+    LANE_IDS();
+    double* r = a.rec + p * a.rec_stride;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) r[(t * 4 + q) * 64 + lane] = T[t][q];
+    r += NT * 256;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) r[(t * 4 + q) * 64 + lane] = Sv[t][q];
+    r += MT * 256;
+#pragma unroll
+    for (int v = 0; v < 5; ++v)
+      for (int i = lane; i < KP; i += 64) r[v * KP + i] = LDS(kvs(rec_kv(v)) + i);
+    r += 5 * KP;
+    for (int i = lane; i < 20 * NCS; i += 64) r[i] = LDS(O_CC + i);
+    if (lane == 0) r[20 * NCS] = sing ? 1.0 : 0.0;  // REC_SING
+  }
+  __device__ __forceinline__ void load_record(int64_t p) {
+    LANE_IDS();
+    const double* r = a.rec + p * a.rec_stride;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) T[t][q] = r[(t * 4 + q) * 64 + lane];
+    r += NT * 256;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Sv[t][q] = r[(t * 4 + q) * 64 + lane];
+    r += MT * 256;
+#pragma unroll
+    for (int v = 0; v < 5; ++v)
+      for (int i = lane; i < KP; i += 64) LDS(kvs(rec_kv(v)) + i) = r[v * KP + i];
+    r += 5 * KP;
+    for (int i = lane; i < 20 * NCS; i += 64) LDS(O_CC + i) = r[i];
+    sing = uni(r[20 * NCS]) != 0.0;
+    SYNC();
+  }
+
   // ------------------------------------------------------------- driver
   // solve_socp (solver.jl:40-153) as a micro-phase loop.  solve_kkt
   // (densesolver.jl:54-90) is MP_SOLVE_HEAD -> MP_SOLVE_MAT -> MP_SOLVE_TAIL;
   // `ret` says which solve it is (init, KKT entry, affine, combined).
+  // KM = 0: the solver kernel (MODE_SOLVE); KM = 1: the plugin-entry kernel
+  // (MODE_KKT, MODE_SETUP, MODE_SOLVEKKT), compiled apart so the solver's
+  // register allocation does not carry the entry paths.
+  template <int KM>
   __device__ __forceinline__ void run(int64_t p) {
+    const int mode = KM ? a.mode : (a.mode == MODE_KKT ? (int)MODE_KKT : (int)MODE_SOLVE);
     STAMP(SP_LOAD);
     dbg_p = p;
     int status = ST_MAXIT, iters = 0, it = 0;
@@ -1849,16 +1918,42 @@ struct Small {
     bool fac_ident = false, fac_aa = false, dm_aa = false;
     int fret = 0, ret = 0, fst = 0;
     int after_singtest;
-    if (a.mode == MODE_KKT) {
-      for (int i = lane; i < k; i += 64) {
-        LDS(S_ + i) = a.s[p * k + i];
-        LDS(Z_ + i) = a.z[p * k + i];
-        LDS(DZ + i) = a.dz[p * k + i];
-        LDS(DS + i) = a.ds[p * k + i];
+    bool have_sing = false;
+    if (mode == MODE_SOLVEKKT) {  // setup_iter failed for this problem: NaN solution, its status
+      const int st0 = (int)uni(a.rec[p * a.rec_stride + REC_STATUS]);
+      if (st0) {
+        for (int j = lane; j < n; j += 64) a.cx[p * n + j] = NAN;
+        for (int i = lane; i < m; i += 64) a.cy[p * m + i] = NAN;
+        for (int i = lane; i < k; i += 64) {
+          a.cz[p * k + i] = NAN;
+          a.cs[p * k + i] = NAN;
+        }
+        if (lane == 0) a.status[p] = st0;
+        return;
       }
-      for (int j = lane; j < n; j += 64) LDS(RD + j) = a.dx[p * n + j];
-      for (int i = lane; i < m; i += 64) LDS(RP + i) = a.dy[p * m + i];
+    }
+    if (mode == MODE_KKT || mode == MODE_SETUP || mode == MODE_SOLVEKKT) {
+      for (int i = lane; i < k; i += 64) {
+        if (mode != MODE_SOLVEKKT) {
+          LDS(S_ + i) = a.s[p * k + i];
+          LDS(Z_ + i) = a.z[p * k + i];
+        }
+        if (mode != MODE_SETUP) {
+          LDS(DZ + i) = a.dz[p * k + i];
+          LDS(DS + i) = a.ds[p * k + i];
+        }
+      }
+      if (mode != MODE_SETUP) {
+        for (int j = lane; j < n; j += 64) LDS(RD + j) = a.dx[p * n + j];
+        for (int i = lane; i < m; i += 64) LDS(RP + i) = a.dy[p * m + i];
+      }
       after_singtest = MP_KKT;
+      if (mode == MODE_SOLVEKKT) {  // solve_kkt against the setup_iter record
+        load_record(p);
+        have_sing = true;
+        after_singtest = MP_SOLVE_HEAD;
+        ret = RET_KKT;
+      }
     } else if (a.flags & F_WARM) {
       for (int j = lane; j < n; j += 64) LDS(X_ + j) = a.x[p * n + j];
       for (int i = lane; i < m; i += 64) LDS(Y_ + i) = a.y[p * m + i];
@@ -1872,7 +1967,9 @@ struct Small {
     }
     SYNC();
     int phase;
-    if (a.sing) {
+    if (have_sing) {
+      phase = after_singtest;
+    } else if (a.sing) {
       sing = uni((int)a.sing[p]) != 0;
       phase = after_singtest;
     } else {
@@ -1882,6 +1979,13 @@ struct Small {
     bool done = false;
     while (!done) {
       LANE_IDS();
+      if (KM && phase == MP_SAVE) {  // setup_iter done: keep the factorisation for the solves
+        // (outside the switch: the solver kernel's phase switch is left as it
+        // was tuned -- an extra case there re-lays the loop and costs ~4%)
+        store_record(p);
+        status = 0;
+        break;
+      }
       int next = phase;
       switch (phase) {
         case MP_SINGTEST:  // Problem's `sing` (Socp.jl:49-56): is G'G positive definite?
@@ -1967,7 +2071,7 @@ struct Small {
           }
           fac_ident = false;
           fac_aa = sing;
-          fret = MP_SOLVE_HEAD;
+          fret = mode == MODE_SETUP ? MP_SAVE : MP_SOLVE_HEAD;
           ret = RET_KKT;
           next = MP_FACTOR;
           break;
@@ -2048,8 +2152,9 @@ struct Small {
       if (done) break;
       phase = uni(next);
     }
-    if (a.mode == MODE_KKT) {
+    if (mode != MODE_SOLVE) {
       if (lane == 0) a.status[p] = status;
+      if (mode == MODE_SETUP && lane == 0) a.rec[p * a.rec_stride + REC_STATUS] = (double)status;
       SYNC();
       STAMP(SP_STORE);
       return;
@@ -2087,7 +2192,7 @@ struct Small {
   }
 };
 
-template <int NQ, int NP, int MQ>
+template <int NQ, int NP, int MQ, int KM>
 __global__ void __launch_bounds__(64, 1) socp_small_kernel(SmallArgs args) {
   Small<NQ, NP, MQ> S(args);
   S.init_tables();
@@ -2098,7 +2203,7 @@ __global__ void __launch_bounds__(64, 1) socp_small_kernel(SmallArgs args) {
     p = __shfl(p, 0);
     if ((int64_t)p >= args.B) break;
     S.load_problem(p);
-    S.run(p);
+    S.template run<KM>(p);
   }
   S.flush_stamps();
 }

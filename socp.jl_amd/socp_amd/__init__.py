@@ -15,6 +15,8 @@ Two layers over libsocp.so (include/socp.h):
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
 from . import _lib
@@ -25,7 +27,8 @@ from ._lib import (CHOL_H_FAILED, CHOL_S_FAILED, CONE_POC, CONE_SOC, CONVERGED, 
 __all__ = [
     "POC", "SOC", "Problem", "State", "Scaling", "DenseSolver", "HipDenseSolver", "SolverState",
     "solve_socp", "solve_socp_batched", "compute_scaling", "setup_iter", "solve_kkt",
-    "PosDefException", "DomainError", "batch_solve", "batch_kkt_solve", "generate", "pack_csc",
+    "PosDefException", "DomainError", "batch_solve", "batch_kkt_solve", "DenseHandle", "generate",
+    "pack_csc",
     "Context", "SocpError", "default_context", "cone_arrays",
     "CONVERGED", "MAXIT", "CHOL_H_FAILED", "CHOL_S_FAILED", "DOMAIN_ERROR",
 ]
@@ -212,6 +215,117 @@ def batch_kkt_solve(cones, n, m, k, A, G, sing, s, z, dx, dy, dz, ds, *, ctx=Non
     return dict(cx=cx, cy=cy[:B * m], cz=cz, cs=cs, status=st)
 
 
+class DenseHandle:
+    """A batch of DenseSolver objects on the device (socp_dense_*): the
+    reference's plugin split (densesolver.jl) -- construction keeps A and G
+    resident (:19-38), ``setup_iter(s, z)`` computes the NT scaling and the
+    factorisation (:41-52) into one record per problem, ``solve_kkt`` solves one
+    right-hand side against it (:54-90) as often as called.
+
+    numpy inputs: every call copies its vectors host-to-device (2k doubles per
+    problem for setup_iter, n+m+2k for solve_kkt; ``h2d_bytes`` reports the last
+    call's count).  torch CUDA inputs (A, G given as tensors): every later
+    argument must be a device tensor too; calls are stream-ordered on torch's
+    current stream.  Results are bitwise those of ``batch_kkt_solve``."""
+
+    def __init__(self, cones, n, m, k, A, G, sing=None, *, ctx=None, force_large=False):
+        L = _lib.load()
+        self.cones, self.n, self.m, self.k = cones, n, m, k
+        self.kind, self.offs, self.dim = cone_arrays(cones)
+        B = _size(G) // (k * n)
+        if B * k * n != _size(G):
+            raise ValueError(f"G: {_size(G)} elements is not a multiple of k*n={k * n}")
+        _check_sizes(B, A=(A if m else None, B * m * n), sing=(sing, B))
+        self.B = B
+        self.ctx = ctx or default_context()
+        self.dev = _is_torch(G)
+        flags = (F_DEVICE_PTRS if self.dev else 0) | (F_FORCE_LARGE if force_large else 0)
+        if self.dev:
+            self.ctx.bind_torch_stream()
+            arrs = (A if m else None, G, sing)
+        else:
+            arrs = (_host(A) if m else None, _host(G), None if sing is None else _host(sing, np.uint8))
+        h = C.c_void_p()
+        dims = _lib.Dims(B, n, m, k, len(self.kind))
+        p = _lib.ptr
+        _lib.check(L.socp_dense_create(self.ctx.handle, dims, p(self.kind), p(self.offs), p(self.dim),
+                                       p(arrs[0]), p(arrs[1]), p(arrs[2]), flags, C.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.load().socp_dense_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _arg(self, a, dtype=np.float64):
+        if self.dev:
+            if not _is_torch(a):
+                raise TypeError("a device handle takes torch CUDA tensors")
+            return a
+        return _host(a, dtype)
+
+    def setup_iter(self, s, z, status=None):
+        """Scaling + factorisation at (s, z); returns the per-problem status
+        (0, CHOL_H_FAILED, CHOL_S_FAILED, DOMAIN_ERROR)."""
+        B, k = self.B, self.k
+        _check_sizes(B, s=(s, B * k), z=(z, B * k))
+        if status is None:
+            if self.dev:
+                import torch
+                status = torch.empty(B, dtype=torch.int32, device=s.device)
+            else:
+                status = np.zeros(B, np.int32)
+        if self.dev:
+            self.ctx.bind_torch_stream()
+        p = _lib.ptr
+        _lib.check(_lib.load().socp_dense_setup_iter(self.handle, p(self._arg(s)), p(self._arg(z)), p(status)))
+        return status
+
+    def solve_kkt(self, dx, dy, dz, ds, out=None):
+        """One KKT solve per problem against the last setup_iter; returns
+        dict(cx, cy, cz, cs, status) (``out`` may supply the arrays)."""
+        B, n, m, k = self.B, self.n, self.m, self.k
+        _check_sizes(B, dx=(dx, B * n), dy=(dy if m else None, B * m), dz=(dz, B * k), ds=(ds, B * k))
+        if out is None:
+            if self.dev:
+                import torch
+                f64 = dict(dtype=torch.float64, device=dz.device)
+                out = dict(cx=torch.empty(B * n, **f64), cy=torch.empty(max(B * m, 1), **f64),
+                           cz=torch.empty(B * k, **f64), cs=torch.empty(B * k, **f64),
+                           status=torch.empty(B, dtype=torch.int32, device=dz.device))
+            else:
+                out = dict(cx=np.zeros(B * n), cy=np.zeros(max(B * m, 1)), cz=np.zeros(B * k),
+                           cs=np.zeros(B * k), status=np.zeros(B, np.int32))
+        if self.dev:
+            self.ctx.bind_torch_stream()
+        p = _lib.ptr
+        _lib.check(_lib.load().socp_dense_solve_kkt(
+            self.handle, p(self._arg(dx)), p(self._arg(dy) if m else None), p(self._arg(dz)),
+            p(self._arg(ds)), p(out["cx"]), p(out["cy"] if m else None), p(out["cz"]), p(out["cs"]),
+            p(out["status"])))
+        if m == 0 or _size(out["cy"]) != B * m:
+            out["cy"] = out["cy"][:B * m]
+        return out
+
+    @property
+    def h2d_bytes(self) -> int:
+        """Host-to-device bytes moved by the last call (socp_dense_h2d_bytes)."""
+        v = C.c_int64()
+        _lib.check(_lib.load().socp_dense_h2d_bytes(self.handle, C.byref(v)))
+        return int(v.value)
+
+    @property
+    def record_bytes(self) -> int:
+        """Device bytes of one problem's factor record."""
+        return int(_lib.load().socp_dense_record_bytes(self.handle))
+
+
 def generate(cones, B, n, m, k, seed, first_problem=0, *, ctx=None, device=None):
     """Device-side generation of B feasible synthetic problems (SURVEY.md §8(d));
     returns torch CUDA tensors (c, A, b, G, h) in the include/socp.h layout."""
@@ -323,8 +437,9 @@ class State:
 
 
 class Scaling:
-    """NT scaling handle (scalings.jl:1-20).  The scaling itself is computed on
-    the GPU inside each KKT call; this object records the (s, z) it is built from."""
+    """NT scaling handle (scalings.jl:1-20), the plugin's AbstractScaling.  The
+    scaling W, W^-1, lambda itself lives on the device, in the DenseSolver's
+    factor record; this object records the (s, z) compute_scaling was given."""
 
     def __init__(self, prob: Problem):
         self.s = np.zeros(prob.k)
@@ -332,30 +447,39 @@ class Scaling:
 
 
 def compute_scaling(cones, scaling: Scaling, s, z):
-    """compute_scaling(cones, scaling, s, z) (scalings.jl:101-110)."""
+    """compute_scaling(cones, scaling, s, z) (scalings.jl:101-110).  The
+    arithmetic runs on the GPU in the next setup_iter (it feeds only that)."""
     scaling.s = np.array(s, dtype=np.float64)
     scaling.z = np.array(z, dtype=np.float64)
     return scaling
 
 
 class DenseSolver:
-    """KKTSolver{Scaling} plugin for the dense path (densesolver.jl:1-90), on MI355X."""
+    """KKTSolver{Scaling} plugin for the dense path (densesolver.jl:1-90) on
+    MI355X: DenseSolver(pr) (:19-38) keeps A and G on the device (a one-problem
+    DenseHandle); setup_iter factors into the handle's record, solve_kkt solves
+    against it, so only n+m+2k doubles move per solve."""
 
     scaling_type = Scaling
 
     def __init__(self, prob: Problem, ctx: Context | None = None):
         self.prob = prob
         self.ctx = ctx
-        self._sz = None
+        self.handle = DenseHandle(prob.cones, prob.n, prob.m, prob.k, _colmajor(prob.A, prob.m, prob.n),
+                                  _colmajor(prob.G, prob.k, prob.n), np.array([prob.sing], np.uint8),
+                                  ctx=ctx)
 
 
 HipDenseSolver = DenseSolver
 
 
 def setup_iter(solver: DenseSolver, prob: Problem, state: State, scaling: Scaling):
-    """setup_iter(::DenseSolver, ...) (densesolver.jl:41-52): the factorisation is
-    fused with the solve on the GPU; this records the iterate it applies to."""
-    solver._sz = (scaling.s.copy(), scaling.z.copy())
+    """setup_iter(::DenseSolver, ...) (densesolver.jl:41-52): scaling, H, H^-1,
+    A H^-1 A' and its factorisation, kept on the device.  Raises
+    PosDefException where cholesky! throws, DomainError where the scaling's
+    sqrt does."""
+    st = solver.handle.setup_iter(scaling.s, scaling.z)
+    _raise_status(int(st[0]))
 
 
 def _raise_status(st):
@@ -367,12 +491,9 @@ def _raise_status(st):
 
 def solve_kkt(solver: DenseSolver, prob: Problem, state: State, scaling: Scaling, dx, dy, dz, ds,
               cx, cy, cz, cs):
-    """solve_kkt(::DenseSolver, ...) (densesolver.jl:54-90): writes (cx,cy,cz,cs)
-    in place and leaves (dx,dy,dz,ds) untouched."""
-    s, z = solver._sz if solver._sz is not None else (scaling.s, scaling.z)
-    out = batch_kkt_solve(prob.cones, prob.n, prob.m, prob.k, _colmajor(prob.A, prob.m, prob.n),
-                          _colmajor(prob.G, prob.k, prob.n), np.array([prob.sing], np.uint8), s, z,
-                          dx, dy, dz, ds, ctx=solver.ctx)
+    """solve_kkt(::DenseSolver, ...) (densesolver.jl:54-90) against the last
+    setup_iter: writes (cx,cy,cz,cs) in place, leaves (dx,dy,dz,ds) untouched."""
+    out = solver.handle.solve_kkt(dx, dy, dz, ds)
     _raise_status(int(out["status"][0]))
     cx[:] = out["cx"]
     cy[:] = out["cy"]

@@ -27,6 +27,8 @@ EXPORTED = [
     "socp_last_kernel_ms", "socp_last_kernel_name", "socp_debug_set_kkt_dump",
     "socp_debug_set_stamps", "socp_pack_csc", "socp_comm_unique_id", "socp_comm_init",
     "socp_comm_destroy", "socp_allgather_status", "socp_allgather_outcomes",
+    "socp_dense_create", "socp_dense_setup_iter", "socp_dense_solve_kkt", "socp_dense_h2d_bytes",
+    "socp_dense_record_bytes", "socp_dense_destroy",
 ]
 
 OUTCOME_BYTES = 32  # sizeof(socp_outcome): int32 status, int32 iters, double rd, rp, gap
@@ -100,6 +102,14 @@ def load():
     L.socp_debug_set_kkt_dump.argtypes = [vp]
     L.socp_debug_set_stamps.argtypes = [vp]
     L.socp_pack_csc.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp, C.c_int32, vp]
+    if hasattr(L, "socp_dense_create"):  # split plugin entries (absent from older A/B builds)
+        L.socp_dense_create.argtypes = common + [dp, dp, u8p, C.c_int32, C.POINTER(C.c_void_p)]
+        L.socp_dense_setup_iter.argtypes = [vp, dp, dp, i32p]
+        L.socp_dense_solve_kkt.argtypes = [vp] + [dp] * 8 + [i32p]
+        L.socp_dense_h2d_bytes.argtypes = [vp, C.POINTER(C.c_int64)]
+        L.socp_dense_record_bytes.argtypes = [vp]
+        L.socp_dense_record_bytes.restype = C.c_int64
+        L.socp_dense_destroy.argtypes = [vp]
     if hasattr(L, "socp_comm_init"):  # RCCL gather (absent from libraries built before it)
         L.socp_comm_unique_id.argtypes = [vp]
         L.socp_comm_init.argtypes = [vp, C.c_int, C.c_int, vp, C.POINTER(C.c_void_p)]
