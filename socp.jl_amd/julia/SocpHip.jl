@@ -1,6 +1,6 @@
 # SocpHip.jl — Julia-side binding of libsocp (include/socp.h) for BenChung/Socp.jl.
 #
-# Drop-in for the dense path: `HipDenseSolver <: KKTSolver{Scaling}` plugs into
+# Drop-in for the dense path: `HipDenseSolver <: KKTSolver{HipScaling}` plugs into
 # the reference's `SolverState(prob, solver)` / `solve_socp(prob, ss)`
 # (solver.jl:22,40), and `solve_socp_batched` runs a whole batch of problems
 # (same dims and cones) in one device call.  All arithmetic happens in the HIP
@@ -8,7 +8,7 @@
 #
 # Usage (inside module Socp, after `include("densesolver.jl")`):
 #     include(joinpath(SOCP_AMD_DIR, "julia", "SocpHip.jl"))
-#     ss = SolverState(prob, HipDenseSolver(prob))
+#     ss = SolverState(prob, HipDenseSolver(prob))           # scaling type: HipScaling
 #     setup_iter(ss.solver, prob, state, scaling)            # densesolver.jl:41
 #     solve_kkt(ss.solver, prob, state, scaling, dx,dy,dz,ds, cx,cy,cz,cs)  # densesolver.jl:54
 #     xs = solve_socp_batched(problems)                       # batched solve_socp
@@ -69,39 +69,124 @@ function socp_throw(st)
 end
 
 # --------------------------------------------------------------- plugin
-mutable struct HipDenseSolver <: KKTSolver{Scaling}
-    A::Matrix{Float64}
-    G::Matrix{Float64}
-    s::Vector{Float64}
-    z::Vector{Float64}
-end
-HipDenseSolver(pr::Problem) = HipDenseSolver(Matrix(pr.A), Matrix(pr.G), zeros(pr.k), zeros(pr.k))
+# HipDenseSolver mirrors DenseSolver's life cycle on the device (include/socp.h,
+# socp_dense_*): construction copies A and G into a one-problem handle once
+# (densesolver.jl:19-38), setup_iter factors into the handle's device record
+# (:41-52), solve_kkt solves against it (:54-90) -- the solver calls it twice per
+# iteration (solver.jl:127,141) -- moving only n+m+2k doubles.
 
-# setup_iter(::DenseSolver) (densesolver.jl:41-52): the factorisation is fused
-# with the solve on the device; record the iterate it applies to.
-function setup_iter(ss::HipDenseSolver, pr::Problem{C,n,m,k,sing}, s::State, scaling::Scaling) where {C,n,m,k,sing}
-    copyto!(ss.s, s.s)
-    copyto!(ss.z, s.z)
+# HipScaling: the lightweight AbstractScaling of the plugin.  SolverState is
+# generic in its scaling type (solver.jl:1-2,22-23: S(pr) for KKTSolver{S}), and
+# the driver loop reads only scaling.l and calls scale!/iscale! (solver.jl:107,
+# 128-129,143-144), which need the per-cone wb and mu -- O(k) data.  The dense
+# W, W^-1 and the k^3 iW*iW' product of the reference's Scaling
+# (scalings.jl:1-20,108) are never formed on the host: the device computes its
+# own NT scaling from (s, z) inside setup_iter.
+struct HipScaling <: AbstractScaling
+    l::Vector{Float64}     # lambda = W z
+    mu::Vector{Float64}    # per cone: sqrt(||s||_J / ||z||_J) (1 for POC)
+    wbs::Vector{Float64}   # POC: sqrt(s/z); SOC: the unit NT vector wb
+end
+HipScaling(p::Problem) = HipScaling(zeros(p.k), zeros(length(p.cones)), zeros(p.k))
+
+function hip_scaling!(c::POC, ci, sc::HipScaling, s, z)
+    for i in cti(c, 1):cti(c, conedim(c))
+        sc.wbs[i] = sqrt(s[i] / z[i])
+        sc.l[i] = sqrt(s[i] * z[i])
+    end
+end
+
+# NT scaling of one second-order cone (scalings.jl:32-99) restated on vectors:
+# normalised s and z, gamma, wb, mu and lambda, no matrices.
+function hip_scaling!(c::SOC, ci, sc::HipScaling, s, z)
+    o, d = cti(c, 1), conedim(c)
+    jz, js = z[o]^2, s[o]^2
+    for i in o+1:o+d-1
+        jz -= z[i] * z[i]
+        js -= s[i] * s[i]
+    end
+    nz, ns = sqrt(jz), sqrt(js)          # DomainError off the cone, like the reference
+    fz, fs = 1 / nz, 1 / ns
+    dot = 0.0
+    for i in o:o+d-1
+        dot += (z[i] * fz) * (s[i] * fs)
+    end
+    gamma = sqrt((1 + dot) / 2)
+    g2 = 1 / (2 * gamma)
+    sc.wbs[o] = (s[o] * fs + z[o] * fz) * g2
+    for i in o+1:o+d-1
+        sc.wbs[i] = (s[i] * fs - z[i] * fz) * g2
+    end
+    sc.mu[ci] = sqrt(ns / nz)
+    z0, s0 = z[o] * fz, s[o] * fs
+    rt = sqrt(ns * nz)
+    mult = rt / (z0 + s0 + 2 * gamma)
+    for i in o+1:o+d-1
+        sc.l[i] = ((s[i] * fs) * (gamma + z0) + (z[i] * fz) * (gamma + s0)) * mult
+    end
+    sc.l[o] = gamma * rt
+end
+
+function compute_scaling(cones::Tuple{Vararg{Cone}}, sc::HipScaling, s, z)
+    for (ci, c) in enumerate(cones)
+        c isa POC && (sc.mu[ci] = 1.0)
+        hip_scaling!(c, ci, sc, s, z)
+    end
+    return sc
+end
+# W s and W^-1 s (scalings.jl:112-160): the per-cone methods read only wbs and mu
+function scale!(cones::Tuple{Vararg{Cone}}, sc::HipScaling, s, op)
+    for (ci, c) in enumerate(cones)
+        scale!(c, ci, sc, s, op)
+    end
+end
+function iscale!(cones::Tuple{Vararg{Cone}}, sc::HipScaling, s, op)
+    for (ci, c) in enumerate(cones)
+        iscale!(c, ci, sc, s, op)
+    end
+end
+
+mutable struct HipDenseSolver <: KKTSolver{HipScaling}
+    handle::Ptr{Cvoid}
+    status::Vector{Int32}
+    function HipDenseSolver(pr::Problem{C,n,m,k,sing}) where {C,n,m,k,sing}
+        kind, offs, dim = cone_arrays(pr.cones)
+        dims = Ref(SocpDims(1, n, m, k, length(pr.cones)))
+        A = Matrix{Float64}(pr.A)   # column-major m x n, as include/socp.h lays it out
+        G = Matrix{Float64}(pr.G)
+        singv = UInt8[sing ? 1 : 0]
+        h = Ref{Ptr{Cvoid}}(C_NULL)
+        socp_check(ccall((:socp_dense_create, libsocp), Cint,
+                         (Ptr{Cvoid}, Ref{SocpDims}, Ptr{Int32}, Ptr{Int32}, Ptr{Int32},
+                          Ptr{Float64}, Ptr{Float64}, Ptr{UInt8}, Int32, Ptr{Ptr{Cvoid}}),
+                         socp_ctx(), dims, kind, offs, dim, A, G, singv, Int32(0), h))
+        ss = new(h[], Int32[0])
+        finalizer(ss) do x
+            x.handle == C_NULL || ccall((:socp_dense_destroy, libsocp), Cint, (Ptr{Cvoid},), x.handle)
+            x.handle = C_NULL
+        end
+        return ss
+    end
+end
+
+# setup_iter(::DenseSolver) (densesolver.jl:41-52): scaling of (s, z), H, H^-1,
+# A H^-1 A' and its factorisation, kept in the handle on the device.
+function setup_iter(ss::HipDenseSolver, pr::Problem{C,n,m,k,sing}, s::State, scaling::HipScaling) where {C,n,m,k,sing}
+    socp_check(ccall((:socp_dense_setup_iter, libsocp), Cint,
+                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}), ss.handle, s.s, s.z, ss.status))
+    socp_throw(ss.status[1])
     return nothing
 end
 
-# solve_kkt(::DenseSolver) (densesolver.jl:54-90): one socp_batch_kkt_solve with batch 1.
-function solve_kkt(ss::HipDenseSolver, pr::Problem{C,n,m,k,sing}, s::State, scaling::Scaling,
+# solve_kkt(::DenseSolver) (densesolver.jl:54-90) against the last setup_iter.
+function solve_kkt(ss::HipDenseSolver, pr::Problem{C,n,m,k,sing}, s::State, scaling::HipScaling,
                    dx::Vector{Float64}, dy::Vector{Float64}, dz::Vector{Float64}, ds::Vector{Float64},
                    cx::Vector{Float64}, cy::Vector{Float64}, cz::Vector{Float64}, cs::Vector{Float64}) where {C,n,m,k,sing}
-    kind, offs, dim = cone_arrays(pr.cones)
-    dims = Ref(SocpDims(1, n, m, k, length(pr.cones)))
-    singv = UInt8[sing ? 1 : 0]
-    st = Int32[0]
-    rc = ccall((:socp_batch_kkt_solve, libsocp), Cint,
-               (Ptr{Cvoid}, Ref{SocpDims}, Ptr{Int32}, Ptr{Int32}, Ptr{Int32},
-                Ptr{Float64}, Ptr{Float64}, Ptr{UInt8}, Ptr{Float64}, Ptr{Float64},
-                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Int32),
-               socp_ctx(), dims, kind, offs, dim, ss.A, ss.G, singv, ss.s, ss.z,
-               dx, dy, dz, ds, cx, cy, cz, cs, st, Int32(0))
-    socp_check(rc)
-    socp_throw(st[1])
+    socp_check(ccall((:socp_dense_solve_kkt, libsocp), Cint,
+                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                      Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                     ss.handle, dx, dy, dz, ds, cx, cy, cz, cs, ss.status))
+    socp_throw(ss.status[1])
     return nothing
 end
 
