@@ -144,6 +144,65 @@ def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None, tol=0.0, structured=
                       + f"{algo}, OpenMP {threads} threads (OMP_NUM_THREADS / affinity), {total_t:.1f}s timed"}
 
 
+def ingest_line(S, cfg, B, K, tol, dev_data, steps, ctx):
+    """PCIe-inclusive rate (never `value`): the same batch held in host memory
+    flows through socp_ingest -- double-buffered pinned staging, batch i+1's
+    host-to-device copy on a copy stream under batch i's solve, results back to
+    the host.  Two forms: inputs already in the pinned slots (zero-copy
+    producer) and inputs in pageable numpy arrays (copied into the slots by
+    submit).  Timed region: `steps` batches submitted two deep, every result on
+    the host at the end."""
+    import numpy as np
+    n, m, k = cfg.n, cfg.m, cfg.k
+    host = [t.cpu().numpy() for t in dev_data]
+    sing = np.zeros(B, np.uint8)
+    ing = S.Ingest(cfg.cones, n, m, k, B, ctx=ctx)
+    kw = dict(maxit=K, tol=tol)
+    views = []
+    for _ in range(2):  # fill both slots once (the solve never writes its inputs)
+        v = ing.next_inputs()
+        for key, arr in zip(("c", "A", "b", "G", "h"), host):
+            v[key][:arr.size] = arr
+        v["sing"][:B] = 0
+        views.append([v[key][:arr.size] for key, arr in zip(("c", "A", "b", "G", "h"), host)] + [v["sing"][:B]])
+        views[-1].append(ing.submit(*views[-1][:6], **kw))
+    it0 = None
+    for v in views:
+        it0 = ing.wait(v.pop())["iters"]
+    iters_per_batch = int(it0.sum())
+
+    def run(src_of):
+        t, outs = [], 0
+        t0 = time.perf_counter()
+        for i in range(steps):
+            if i >= 2:
+                ing.wait(t[i - 2])
+                outs += 1
+            t.append(ing.submit(*src_of(i), **kw))
+        for tk in t[outs:]:
+            ing.wait(tk)
+        return time.perf_counter() - t0
+
+    dt_pin = run(lambda i: views[i % 2])
+    dt_page = run(lambda i: host + [sing])
+    in_bytes = 8 * B * (n + m * n + m + k * n + k) + B
+    out_bytes = 8 * B * (n + m + 2 * k) + 4 * 2 * B + 8 * 3 * B
+    ing.close()
+    return {
+        "value": iters_per_batch * steps / dt_pin,
+        "unit": "problem-iterations/s",
+        "ms_per_batch": dt_pin / steps * 1e3,
+        "h2d_bytes_per_batch": in_bytes,
+        "d2h_bytes_per_batch": out_bytes,
+        "h2d_GBps": in_bytes * steps / dt_pin / 1e9,
+        "pageable": {"value": iters_per_batch * steps / dt_page, "ms_per_batch": dt_page / steps * 1e3,
+                     "h2d_GBps": in_bytes * steps / dt_page / 1e9},
+        "mode": "socp_ingest: host batch -> pinned slot -> H2D (copy stream) overlapped with the previous "
+                "batch's solve -> D2H; `value` = inputs already in pinned slots, `pageable` = inputs in "
+                "numpy arrays copied into the slots by submit",
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,6 +216,8 @@ def main():
                          "reference's stopping rule, tol=1e-5 absolute, maxit=40, per-problem masking (§8(d)(ii))")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="per CPU line (two lines)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ingest", action="store_true",
+                    help="skip the PCIe-inclusive line (host batches through socp_ingest, N=1 only)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default: the newest profiles/rNN_pmc_traffic[_<config>].json")
     args = ap.parse_args()
@@ -287,6 +348,8 @@ def main():
                 "problem_iters_per_launch": iters_per_launch,
             },
         }
+        if world == 1 and not args.no_ingest:
+            line["ingest"] = ingest_line(S, cfg, B, K, tol, (c, A, b, G, h), args.steps, ctx)
         if not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol)
             line["cpu_baseline_structured"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol,

@@ -228,6 +228,49 @@ int socp_pack_csc(socp_ctx* ctx, int64_t batch, int32_t rows, int32_t cols,
                   const int64_t* nz_offs, const int64_t* colptr, const int64_t* rowval,
                   const double* nzval, int32_t index_base, double* dense);
 
+/* Pipelined ingest of host-resident batches: the
+ * reference builds each Problem on the host (Socp.jl:20-60); here a stream of
+ * host batches flows through two slots of pinned (hipHostMalloc) staging so
+ * batch i+1's host-to-device copy -- and, in the CSC form, its packing --
+ * runs on a copy stream while batch i solves on the context's stream, and
+ * batch i's results drain to pinned memory on a third stream.
+ *   socp_ingest_create(ctx, dims, cones..., flags, &ing): dims.batch is the
+ *       largest batch one submit may carry (pinned + device space for two
+ *       such batches is allocated here); flags: SOCP_F_FORCE_LARGE.
+ *   socp_ingest_submit(ing, B, c, A, b, G, h, sing, params, &ticket): host
+ *       arrays in the batch layout above, copied into the slot's pinned
+ *       block (no copy for arrays already written at the pointers
+ *       socp_ingest_next_inputs returns), then everything is asynchronous.
+ *       params->flags other than the defaults are ignored (no warm start).
+ *   socp_ingest_submit_csc(...): A and G as the SparseMatrixCSC arrays of
+ *       socp_pack_csc (host pointers; nz_offs[B] - nz_offs[0] nonzeros each),
+ *       packed on the device on the copy stream.
+ *   socp_ingest_wait(ing, ticket, x, y, z, s, iters, status, res): blocks
+ *       until that batch's results are on the host and copies them out (res
+ *       may be NULL).  A CSC batch with bad indices returns SOCP_E_INVALID here.
+ * At most two tickets are outstanding: a third submit before the oldest is
+ * waited for returns SOCP_E_INVALID.  Results are bitwise those of
+ * socp_batch_solve_ex on the same inputs. */
+typedef struct socp_ingest socp_ingest;
+int socp_ingest_create(socp_ctx* ctx, const socp_dims* dims,
+                       const int32_t* cone_kind, const int32_t* cone_offs, const int32_t* cone_dim,
+                       int32_t flags, socp_ingest** out);
+int socp_ingest_next_inputs(socp_ingest* ing, double** c, double** A, double** b, double** G,
+                            double** h, uint8_t** sing);
+int socp_ingest_submit(socp_ingest* ing, int64_t batch, const double* c, const double* A,
+                       const double* b, const double* G, const double* h, const uint8_t* sing,
+                       const socp_params* params, int64_t* ticket);
+int socp_ingest_submit_csc(socp_ingest* ing, int64_t batch, const double* c, const double* b,
+                           const double* h, const uint8_t* sing,
+                           const int64_t* A_nz_offs, const int64_t* A_colptr, const int64_t* A_rowval,
+                           const double* A_nzval,
+                           const int64_t* G_nz_offs, const int64_t* G_colptr, const int64_t* G_rowval,
+                           const double* G_nzval, int32_t index_base, const socp_params* params,
+                           int64_t* ticket);
+int socp_ingest_wait(socp_ingest* ing, int64_t ticket, double* x, double* y, double* z, double* s,
+                     int32_t* iters, int32_t* status, double* res);
+int socp_ingest_destroy(socp_ingest* ing);
+
 /* Multi-GPU outcome gather: problems shard across ranks
  * (one process per GPU) with no data-path exchange; the only collective is the
  * all-gather of each problem's (status, iters) over RCCL (xGMI between the

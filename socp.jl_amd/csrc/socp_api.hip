@@ -11,6 +11,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/socp.h"
@@ -998,6 +999,418 @@ extern "C" int socp_pack_csc(socp_ctx* ctx, int64_t batch, int32_t rows, int32_t
   HIPCHK(hipStreamSynchronize(ctx->stream));
   if (herr & 1) return fail(SOCP_E_INVALID, "colptr does not span the problem's nonzeros");
   if (herr & 2) return fail(SOCP_E_INVALID, "row index out of range");
+  return 0;
+}
+
+// ------------------------------------------------------- pipelined ingest
+// socp_ingest: host batches -> pinned staging -> device -> solve -> host, with
+// two slots so batch i+1's host-to-device copy (and CSC packing) runs on a copy
+// stream while batch i solves on the context's stream, and batch i's results
+// drain on a third stream.  Per slot: one pinned input block, one pinned output
+// block, device buffers, and three events (inputs on the device, solved,
+// outputs on the host).
+namespace {
+constexpr size_t kAl = 256;
+inline size_t al_up(size_t v) { return (v + kAl - 1) / kAl * kAl; }
+
+struct IngestSlot {
+  void* pin_in = nullptr;
+  void* pin_out = nullptr;
+  size_t pin_in_cap = 0, pin_out_cap = 0;
+  DevBuf dev_in, dev_out, dev_csc;
+  hipEvent_t ready = nullptr, solved = nullptr, done = nullptr;
+  int64_t ticket = -1;  // outstanding ticket, -1 when free
+  int64_t batch = 0;
+  bool csc = false;
+};
+
+// parallel host copy into pinned staging (a single thread reaches ~10 GB/s,
+// well below PCIe; larger copies are split over up to 8 threads)
+void par_copy(void* dst, const void* src, size_t bytes) {
+  if (!src || !bytes || dst == src) return;
+  const size_t chunk = 64ull << 20;
+  const unsigned nt = (unsigned)std::min<size_t>(8, (bytes + chunk - 1) / chunk);
+  if (nt <= 1) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (bytes + nt - 1) / nt;
+  for (unsigned t = 0; t < nt; ++t) {
+    const size_t o = (size_t)t * per;
+    if (o >= bytes) break;
+    const size_t len = std::min(per, bytes - o);
+    th.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, len); });
+  }
+  for (auto& t : th) t.join();
+}
+}  // namespace
+
+struct socp_ingest {
+  socp_ctx* ctx = nullptr;
+  socp_dims dims;  // dims.batch = the largest batch a submit may carry
+  ConeTable cones;
+  int degree = 0;
+  int32_t flags = 0;
+  const SmallVariant* v = nullptr;
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  IngestSlot slot[2];
+  int64_t next = 0;
+  DevBuf counter, err;
+};
+
+// the byte layout of one slot's blocks for `B` problems
+struct InLayout {
+  size_t c, A, b, G, h, sing, total;
+};
+static InLayout in_layout(const socp_dims& d, int64_t B) {
+  InLayout L;
+  size_t o = 0;
+  L.c = o;    o += al_up(sizeof(double) * B * d.n);
+  L.A = o;    o += al_up(sizeof(double) * B * d.m * d.n);
+  L.b = o;    o += al_up(sizeof(double) * B * d.m);
+  L.G = o;    o += al_up(sizeof(double) * B * d.k * d.n);
+  L.h = o;    o += al_up(sizeof(double) * B * d.k);
+  L.sing = o; o += al_up((size_t)B);
+  L.total = o;
+  return L;
+}
+struct OutLayout {
+  size_t x, y, z, s, it, st, res, err, total;
+};
+static OutLayout out_layout(const socp_dims& d, int64_t B) {
+  OutLayout L;
+  size_t o = 0;
+  L.x = o;   o += al_up(sizeof(double) * B * d.n);
+  L.y = o;   o += al_up(sizeof(double) * B * d.m);
+  L.z = o;   o += al_up(sizeof(double) * B * d.k);
+  L.s = o;   o += al_up(sizeof(double) * B * d.k);
+  L.it = o;  o += al_up(sizeof(int32_t) * B);
+  L.st = o;  o += al_up(sizeof(int32_t) * B);
+  L.res = o; o += al_up(sizeof(double) * 3 * B);
+  L.err = o; o += kAl;
+  L.total = o;
+  return L;
+}
+
+static void ingest_free(socp_ingest* g) {
+  if (!g) return;
+  (void)hipSetDevice(g->ctx->device);
+  if (g->h2d) (void)hipStreamSynchronize(g->h2d);
+  (void)hipStreamSynchronize(g->ctx->stream);
+  if (g->d2h) (void)hipStreamSynchronize(g->d2h);
+  for (auto& sl : g->slot) {
+    if (sl.pin_in) (void)hipHostFree(sl.pin_in);
+    if (sl.pin_out) (void)hipHostFree(sl.pin_out);
+    sl.dev_in.release();
+    sl.dev_out.release();
+    sl.dev_csc.release();
+    if (sl.ready) (void)hipEventDestroy(sl.ready);
+    if (sl.solved) (void)hipEventDestroy(sl.solved);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
+  g->counter.release();
+  g->err.release();
+  if (g->h2d) (void)hipStreamDestroy(g->h2d);
+  if (g->d2h) (void)hipStreamDestroy(g->d2h);
+  delete g;
+}
+
+extern "C" int socp_ingest_create(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,
+                                  const int32_t* cone_offs, const int32_t* cone_dim, int32_t flags,
+                                  socp_ingest** out) {
+  if (!out) return fail(SOCP_E_INVALID, "out is NULL");
+  *out = nullptr;
+  if (!ctx) return fail(SOCP_E_INVALID, "ctx is NULL");
+  socp_ingest* g = new socp_ingest();
+  g->ctx = ctx;
+  auto bail = [&](int rc) {
+    ingest_free(g);
+    return rc;
+  };
+  int rc = check_problem(dims, cone_kind, cone_offs, cone_dim, &g->cones, &g->degree);
+  if (rc) return bail(rc);
+  g->dims = *dims;
+  g->flags = flags & SOCP_F_FORCE_LARGE;
+  const int n = dims->n, m = dims->m, k = dims->k;
+  g->v = ((flags & SOCP_F_FORCE_LARGE) || dims->ncones > NCS) ? nullptr : pick_variant(n, m, k);
+  if (!g->v && !large_fits(n, m, k, dims->ncones, nullptr)) return bail(fail(SOCP_E_UNSUPPORTED, kUnsupported));
+  hipError_t e;
+  if ((e = hipSetDevice(ctx->device)) != hipSuccess) return bail(fail(SOCP_E_HIP, "hipSetDevice"));
+  if ((e = hipStreamCreateWithFlags(&g->h2d, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&g->d2h, hipStreamNonBlocking)) != hipSuccess)
+    return bail(fail(SOCP_E_HIP, std::string("hipStreamCreateWithFlags: ") + hipGetErrorString(e)));
+  const int64_t B = dims->batch;
+  const InLayout Li = in_layout(*dims, B);
+  const OutLayout Lo = out_layout(*dims, B);
+  for (auto& sl : g->slot) {
+    if (hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sl.solved, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess)
+      return bail(fail(SOCP_E_HIP, "hipEventCreate"));
+    if (hipHostMalloc(&sl.pin_in, Li.total, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&sl.pin_out, Lo.total, hipHostMallocDefault) != hipSuccess)
+      return bail(fail(SOCP_E_NOMEM, "pinned host allocation failed"));
+    sl.pin_in_cap = Li.total;
+    sl.pin_out_cap = Lo.total;
+    if (sl.dev_in.ensure(Li.total) || sl.dev_out.ensure(Lo.total))
+      return bail(fail(SOCP_E_NOMEM, "device allocation failed"));
+  }
+  if (g->counter.ensure(256) || g->err.ensure(256)) return bail(fail(SOCP_E_NOMEM, "device allocation failed"));
+  *out = g;
+  return 0;
+}
+
+extern "C" int socp_ingest_destroy(socp_ingest* g) {
+  ingest_free(g);
+  return 0;
+}
+
+// pinned input arrays of the slot the next submit will use: a producer that
+// writes there directly saves the host copy (submit sees its own pointers)
+extern "C" int socp_ingest_next_inputs(socp_ingest* g, double** c, double** A, double** b, double** G,
+                                       double** h, uint8_t** sing) {
+  if (!g) return fail(SOCP_E_INVALID, "ingest is NULL");
+  IngestSlot& sl = g->slot[g->next & 1];
+  if (sl.ticket >= 0) return fail(SOCP_E_INVALID, "the next slot is busy: wait for its ticket first");
+  const InLayout L = in_layout(g->dims, g->dims.batch);
+  char* base = (char*)sl.pin_in;
+  if (c) *c = (double*)(base + L.c);
+  if (A) *A = (double*)(base + L.A);
+  if (b) *b = (double*)(base + L.b);
+  if (G) *G = (double*)(base + L.G);
+  if (h) *h = (double*)(base + L.h);
+  if (sing) *sing = (uint8_t*)(base + L.sing);
+  return 0;
+}
+
+// the part of submit shared by the dense and CSC forms: the slot's solve on the
+// context's stream after `ready`, and the result copies on the d2h stream
+static int ingest_solve(socp_ingest* g, IngestSlot& sl, int64_t B, const uint8_t* sing_dev, bool have_sing,
+                        const socp_params* params, const double* A_dev, const double* G_dev) {
+  socp_ctx* ctx = g->ctx;
+  const socp_dims& d = g->dims;
+  const InLayout Li = in_layout(d, d.batch);
+  const OutLayout Lo = out_layout(d, d.batch);
+  char* din = (char*)sl.dev_in.p;
+  char* dout = (char*)sl.dev_out.p;
+  socp_params P;
+  if (params)
+    P = *params;
+  else
+    socp_params_default(&P);
+  SmallArgs a;
+  memset(&a, 0, sizeof(a));
+  a.cones = g->cones;
+  a.B = B;
+  a.n = d.n;
+  a.m = d.m;
+  a.k = d.k;
+  a.nc = d.ncones;
+  a.maxit = P.maxit;
+  a.sigma_exp = P.sigma_exp;
+  a.tol = P.tol;
+  a.step = P.step;
+  a.init_eps = P.init_eps;
+  a.flags = P.flags & ~SOCP_F_WARM_START;
+  a.mode = MODE_SOLVE;
+  a.deg = g->degree;
+  a.c = (const double*)(din + Li.c);
+  a.A = d.m > 0 ? A_dev : nullptr;
+  a.b = (const double*)(din + Li.b);
+  a.G = G_dev;
+  a.h = (const double*)(din + Li.h);
+  a.sing = have_sing ? sing_dev : nullptr;
+  a.x = (double*)(dout + Lo.x);
+  a.y = (double*)(dout + Lo.y);
+  a.z = (double*)(dout + Lo.z);
+  a.s = (double*)(dout + Lo.s);
+  a.iters = (int32_t*)(dout + Lo.it);
+  a.status = (int32_t*)(dout + Lo.st);
+  a.res = (double*)(dout + Lo.res);
+  a.counter = (int32_t*)g->counter.p;
+  HIPCHK(hipStreamWaitEvent(ctx->stream, sl.ready, 0));
+  TRY(g->v ? launch_small(ctx, a, g->v) : launch_large(ctx, a));
+  HIPCHK(hipEventRecord(sl.solved, ctx->stream));
+  HIPCHK(hipStreamWaitEvent(g->d2h, sl.solved, 0));
+  // one copy of the whole output block (x y z s iters status res err)
+  const size_t used = Lo.total;
+  HIPCHK(hipMemcpyAsync(sl.pin_out, dout, used, hipMemcpyDeviceToHost, g->d2h));
+  HIPCHK(hipEventRecord(sl.done, g->d2h));
+  return 0;
+}
+
+static int ingest_begin(socp_ingest* g, int64_t batch, IngestSlot** out) {
+  if (!g) return fail(SOCP_E_INVALID, "ingest is NULL");
+  if (batch < 0 || batch > g->dims.batch) return fail(SOCP_E_INVALID, "batch outside 0..max_batch of the ingest");
+  IngestSlot& sl = g->slot[g->next & 1];
+  if (sl.ticket >= 0) return fail(SOCP_E_INVALID, "two tickets outstanding: wait for the older one first");
+  HIPCHK(hipSetDevice(g->ctx->device));
+  *out = &sl;
+  return 0;
+}
+
+extern "C" int socp_ingest_submit(socp_ingest* g, int64_t batch, const double* c, const double* A, const double* b,
+                                  const double* G, const double* h, const uint8_t* sing, const socp_params* params,
+                                  int64_t* ticket) {
+  IngestSlot* slp = nullptr;
+  TRY(ingest_begin(g, batch, &slp));
+  IngestSlot& sl = *slp;
+  const socp_dims& d = g->dims;
+  const int64_t B = batch;
+  if (!ticket) return fail(SOCP_E_INVALID, "ticket is NULL");
+  if (B > 0 && (!c || !G || !h || (d.m > 0 && (!A || !b)))) return fail(SOCP_E_INVALID, "NULL data pointer");
+  const InLayout L = in_layout(d, d.batch);
+  char* pin = (char*)sl.pin_in;
+  char* din = (char*)sl.dev_in.p;
+  // host -> pinned (skipped for arrays already written into the slot)
+  const size_t nb[6] = {sizeof(double) * B * d.n, sizeof(double) * B * d.m * d.n, sizeof(double) * B * d.m,
+                        sizeof(double) * B * d.k * d.n, sizeof(double) * B * d.k, (size_t)B};
+  const size_t off[6] = {L.c, L.A, L.b, L.G, L.h, L.sing};
+  const void* src[6] = {c, A, b, G, h, sing};
+  for (int i = 0; i < 6; ++i) par_copy(pin + off[i], src[i], nb[i]);
+  // pinned -> device on the copy stream: one transfer per array
+  for (int i = 0; i < 6; ++i)
+    if (src[i] && nb[i]) HIPCHK(hipMemcpyAsync(din + off[i], pin + off[i], nb[i], hipMemcpyHostToDevice, g->h2d));
+  HIPCHK(hipEventRecord(sl.ready, g->h2d));
+  if (B > 0)
+    TRY(ingest_solve(g, sl, B, (const uint8_t*)(din + L.sing), sing != nullptr, params,
+                     (const double*)(din + L.A), (const double*)(din + L.G)));
+  sl.ticket = g->next++;
+  sl.batch = B;
+  sl.csc = false;
+  *ticket = sl.ticket;
+  return 0;
+}
+
+// CSC form: A and G arrive as the SparseMatrixCSC arrays of socp_pack_csc;
+// they are copied to the device and packed there on the copy stream
+extern "C" int socp_ingest_submit_csc(socp_ingest* g, int64_t batch, const double* c, const double* b,
+                                      const double* h, const uint8_t* sing, const int64_t* A_nz_offs,
+                                      const int64_t* A_colptr, const int64_t* A_rowval, const double* A_nzval,
+                                      const int64_t* G_nz_offs, const int64_t* G_colptr, const int64_t* G_rowval,
+                                      const double* G_nzval, int32_t index_base, const socp_params* params,
+                                      int64_t* ticket) {
+  IngestSlot* slp = nullptr;
+  TRY(ingest_begin(g, batch, &slp));
+  IngestSlot& sl = *slp;
+  const socp_dims& d = g->dims;
+  const int64_t B = batch;
+  if (!ticket) return fail(SOCP_E_INVALID, "ticket is NULL");
+  if (index_base != 0 && index_base != 1) return fail(SOCP_E_INVALID, "index_base must be 0 or 1");
+  if (B > 0 && (!c || !h || !G_nz_offs || !G_colptr || (d.m > 0 && (!b || !A_nz_offs || !A_colptr))))
+    return fail(SOCP_E_INVALID, "NULL data pointer");
+  const InLayout L = in_layout(d, d.batch);
+  char* pin = (char*)sl.pin_in;
+  char* din = (char*)sl.dev_in.p;
+  const size_t nb[4] = {sizeof(double) * B * d.n, sizeof(double) * B * d.m, sizeof(double) * B * d.k, (size_t)B};
+  const size_t off[4] = {L.c, L.b, L.h, L.sing};
+  const void* src[4] = {c, b, h, sing};
+  for (int i = 0; i < 4; ++i) par_copy(pin + off[i], src[i], nb[i]);
+  for (int i = 0; i < 4; ++i)
+    if (src[i] && nb[i]) HIPCHK(hipMemcpyAsync(din + off[i], pin + off[i], nb[i], hipMemcpyHostToDevice, g->h2d));
+  // the CSC arrays: sizes from the host offsets; staged through the slot's
+  // pinned output block's tail would race with results, so they get pinned
+  // space of their own after the dense inputs (grown on demand)
+  const int64_t nzA = (d.m > 0 && B > 0) ? A_nz_offs[B] - A_nz_offs[0] : 0;
+  const int64_t nzG = B > 0 ? G_nz_offs[B] - G_nz_offs[0] : 0;
+  if (nzA < 0 || nzG < 0) return fail(SOCP_E_INVALID, "nz_offs must be non-decreasing");
+  const size_t cA = (size_t)(d.n + 1), cG = (size_t)(d.n + 1);
+  size_t o = 0;
+  const size_t oAo = o;  o += al_up(sizeof(int64_t) * (B + 1));
+  const size_t oAc = o;  o += al_up(sizeof(int64_t) * B * cA);
+  const size_t oAr = o;  o += al_up(sizeof(int64_t) * (nzA + 1));
+  const size_t oAv = o;  o += al_up(sizeof(double) * (nzA + 1));
+  const size_t oGo = o;  o += al_up(sizeof(int64_t) * (B + 1));
+  const size_t oGc = o;  o += al_up(sizeof(int64_t) * B * cG);
+  const size_t oGr = o;  o += al_up(sizeof(int64_t) * (nzG + 1));
+  const size_t oGv = o;  o += al_up(sizeof(double) * (nzG + 1));
+  const size_t csc_bytes = o;
+  // pinned CSC staging: the input block is regrown (its dense part re-copied)
+  if (L.total + csc_bytes > sl.pin_in_cap) {
+    void* np = nullptr;
+    if (hipHostMalloc(&np, L.total + csc_bytes, hipHostMallocDefault) != hipSuccess)
+      return fail(SOCP_E_NOMEM, "pinned host allocation failed");
+    HIPCHK(hipStreamSynchronize(g->h2d));  // the dense copies above read the old block
+    memcpy(np, sl.pin_in, L.total);
+    (void)hipHostFree(sl.pin_in);
+    sl.pin_in = np;
+    sl.pin_in_cap = L.total + csc_bytes;
+    pin = (char*)sl.pin_in;
+  }
+  // device: the CSC arrays, then the dense A and G they are packed into
+  const size_t dA = al_up(sizeof(double) * B * d.m * d.n), dG = al_up(sizeof(double) * B * d.k * d.n);
+  if (sl.dev_csc.ensure(csc_bytes + dA + dG)) return fail(SOCP_E_NOMEM, "device allocation failed");
+  char* pc = pin + L.total;
+  char* dc = (char*)sl.dev_csc.p;
+  // offsets are rebased to start at 0 for the pack kernel
+  auto put_offs = [&](size_t off_, const int64_t* v) {
+    int64_t* t = (int64_t*)(pc + off_);
+    for (int64_t p = 0; p <= B; ++p) t[p] = v[p] - v[0];
+  };
+  if (d.m > 0 && B > 0) {
+    put_offs(oAo, A_nz_offs);
+    par_copy(pc + oAc, A_colptr, sizeof(int64_t) * B * cA);
+    par_copy(pc + oAr, A_rowval + 0, sizeof(int64_t) * nzA);
+    par_copy(pc + oAv, A_nzval + 0, sizeof(double) * nzA);
+  }
+  if (B > 0) {
+    put_offs(oGo, G_nz_offs);
+    par_copy(pc + oGc, G_colptr, sizeof(int64_t) * B * cG);
+    par_copy(pc + oGr, G_rowval, sizeof(int64_t) * nzG);
+    par_copy(pc + oGv, G_nzval, sizeof(double) * nzG);
+  }
+  if (B > 0) HIPCHK(hipMemcpyAsync(dc, pc, csc_bytes, hipMemcpyHostToDevice, g->h2d));
+  double* A_dev = (double*)(dc + csc_bytes);
+  double* G_dev = (double*)(dc + csc_bytes + dA);
+  int32_t* err = (int32_t*)((char*)sl.dev_out.p + out_layout(d, d.batch).err);
+  HIPCHK(hipMemsetAsync(err, 0, sizeof(int32_t), g->h2d));
+  if (B > 0 && d.m > 0)
+    hipLaunchKernelGGL(socp_pack_csc_kernel, dim3((unsigned)B), dim3(256), 0, g->h2d, d.m, d.n,
+                       (const int64_t*)(dc + oAo), (const int64_t*)(dc + oAc), (const int64_t*)(dc + oAr),
+                       (const double*)(dc + oAv), (int64_t)index_base, A_dev, err);
+  if (B > 0)
+    hipLaunchKernelGGL(socp_pack_csc_kernel, dim3((unsigned)B), dim3(256), 0, g->h2d, d.k, d.n,
+                       (const int64_t*)(dc + oGo), (const int64_t*)(dc + oGc), (const int64_t*)(dc + oGr),
+                       (const double*)(dc + oGv), (int64_t)index_base, G_dev, err);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(sl.ready, g->h2d));
+  if (B > 0) TRY(ingest_solve(g, sl, B, (const uint8_t*)(din + L.sing), sing != nullptr, params, A_dev, G_dev));
+  sl.ticket = g->next++;
+  sl.batch = B;
+  sl.csc = true;
+  *ticket = sl.ticket;
+  return 0;
+}
+
+extern "C" int socp_ingest_wait(socp_ingest* g, int64_t ticket, double* x, double* y, double* z, double* s,
+                                int32_t* iters, int32_t* status, double* res) {
+  if (!g) return fail(SOCP_E_INVALID, "ingest is NULL");
+  IngestSlot* slp = nullptr;
+  for (auto& sl : g->slot)
+    if (sl.ticket == ticket && ticket >= 0) slp = &sl;
+  if (!slp) return fail(SOCP_E_INVALID, "unknown or already collected ticket");
+  IngestSlot& sl = *slp;
+  HIPCHK(hipSetDevice(g->ctx->device));
+  sl.ticket = -1;  // the slot is free again whatever happens below
+  if (sl.batch == 0) return 0;
+  HIPCHK(hipEventSynchronize(sl.done));
+  const socp_dims& d = g->dims;
+  const int64_t B = sl.batch;
+  const OutLayout L = out_layout(d, d.batch);
+  const char* po = (const char*)sl.pin_out;
+  if (sl.csc) {
+    const int32_t herr = *(const int32_t*)(po + L.err);
+    if (herr & 1) return fail(SOCP_E_INVALID, "colptr does not span the problem's nonzeros");
+    if (herr & 2) return fail(SOCP_E_INVALID, "row index out of range");
+  }
+  par_copy(x, po + L.x, sizeof(double) * B * d.n);
+  if (y) par_copy(y, po + L.y, sizeof(double) * B * d.m);
+  par_copy(z, po + L.z, sizeof(double) * B * d.k);
+  par_copy(s, po + L.s, sizeof(double) * B * d.k);
+  if (iters) memcpy(iters, po + L.it, sizeof(int32_t) * B);
+  if (status) memcpy(status, po + L.st, sizeof(int32_t) * B);
+  if (res) memcpy(res, po + L.res, sizeof(double) * 3 * B);
   return 0;
 }
 

@@ -27,8 +27,8 @@ from ._lib import (CHOL_H_FAILED, CHOL_S_FAILED, CONE_POC, CONE_SOC, CONVERGED, 
 __all__ = [
     "POC", "SOC", "Problem", "State", "Scaling", "DenseSolver", "HipDenseSolver", "SolverState",
     "solve_socp", "solve_socp_batched", "compute_scaling", "setup_iter", "solve_kkt",
-    "PosDefException", "DomainError", "batch_solve", "batch_kkt_solve", "DenseHandle", "generate",
-    "pack_csc",
+    "PosDefException", "DomainError", "batch_solve", "batch_kkt_solve", "DenseHandle", "Ingest",
+    "generate", "pack_csc",
     "Context", "SocpError", "default_context", "cone_arrays",
     "CONVERGED", "MAXIT", "CHOL_H_FAILED", "CHOL_S_FAILED", "DOMAIN_ERROR",
 ]
@@ -324,6 +324,123 @@ class DenseHandle:
     def record_bytes(self) -> int:
         """Device bytes of one problem's factor record."""
         return int(_lib.load().socp_dense_record_bytes(self.handle))
+
+
+def _csc_arrays(mats, rows, cols, index_base):
+    """(nz_offs, colptr, rowval, nzval) host arrays of a list of scipy.sparse
+    matrices in canonical CSC form (sorted, duplicates summed)."""
+    csc = []
+    for M in mats:
+        M = M.tocsc(copy=True)
+        M.sum_duplicates()
+        if M.shape != (rows, cols):
+            raise ValueError(f"matrix shape {M.shape}, expected {(rows, cols)}")
+        csc.append(M)
+    nz = np.cumsum(np.array([0] + [M.nnz for M in csc], dtype=np.int64))
+    colptr = (np.concatenate([M.indptr.astype(np.int64) + index_base for M in csc]) if csc
+              else np.zeros(1, np.int64))
+    rowval = (np.concatenate([M.indices.astype(np.int64) + index_base for M in csc]) if nz[-1]
+              else np.zeros(1, np.int64))
+    nzval = np.concatenate([M.data.astype(np.float64) for M in csc]) if nz[-1] else np.zeros(1)
+    return nz, colptr, rowval, nzval
+
+
+class Ingest:
+    """Pipelined host ingest (socp_ingest_*): host batches through two slots of
+    pinned staging, batch i+1's host-to-device copy (and CSC packing) overlapping
+    batch i's solve.  ``submit`` / ``submit_csc`` return a ticket, ``wait``
+    returns the batch_solve dict; at most two tickets are outstanding.
+    ``next_inputs()`` gives numpy views of the next slot's pinned input arrays
+    (a producer filling them in place saves the host copy)."""
+
+    def __init__(self, cones, n, m, k, max_batch, *, ctx=None, force_large=False):
+        L = _lib.load()
+        self.cones, self.n, self.m, self.k, self.max_batch = cones, n, m, k, int(max_batch)
+        self.kind, self.offs, self.dim = cone_arrays(cones)
+        self.ctx = ctx or default_context()
+        h = C.c_void_p()
+        dims = _lib.Dims(self.max_batch, n, m, k, len(self.kind))
+        p = _lib.ptr
+        _lib.check(L.socp_ingest_create(self.ctx.handle, dims, p(self.kind), p(self.offs), p(self.dim),
+                                        F_FORCE_LARGE if force_large else 0, C.byref(h)))
+        self.handle = h
+        self._batch = {}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.load().socp_ingest_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def next_inputs(self):
+        ptrs = [C.c_void_p() for _ in range(6)]
+        _lib.check(_lib.load().socp_ingest_next_inputs(self.handle, *[C.byref(q) for q in ptrs]))
+        B, n, m, k = self.max_batch, self.n, self.m, self.k
+        out = {}
+        for key, q, cnt, ct in zip(("c", "A", "b", "G", "h", "sing"), ptrs,
+                                   (B * n, B * m * n, B * m, B * k * n, B * k, B),
+                                   (C.c_double,) * 5 + (C.c_uint8,)):
+            out[key] = np.ctypeslib.as_array(C.cast(q, C.POINTER(ct)), shape=(max(cnt, 1),))[:cnt]
+        return out
+
+    def _params(self, maxit, tol, step, sigma_exp, init_eps):
+        return default_params(maxit=maxit, tol=tol, step=step, sigma_exp=sigma_exp, init_eps=init_eps)
+
+    def submit(self, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5, step=0.99, sigma_exp=3, init_eps=1e-10):
+        n, m, k = self.n, self.m, self.k
+        B = np.size(c) // n
+        _check_sizes(B, c=(c, B * n), A=(A if m else None, B * m * n), b=(b if m else None, B * m),
+                     G=(G, B * k * n), h=(h, B * k), sing=(sing, B))
+        t = C.c_int64()
+        P = self._params(maxit, tol, step, sigma_exp, init_eps)
+        p = _lib.ptr
+        arr = [_host(c), _host(A) if m else None, _host(b) if m else None, _host(G), _host(h),
+               None if sing is None else _host(sing, np.uint8)]
+        _lib.check(_lib.load().socp_ingest_submit(self.handle, B, *[p(a) for a in arr], P, C.byref(t)))
+        self._batch[t.value] = B
+        return t.value
+
+    def submit_csc(self, c, b, h, sing, A_mats, G_mats, *, index_base=1, maxit=40, tol=1e-5, step=0.99,
+                   sigma_exp=3, init_eps=1e-10):
+        """A_mats, G_mats: lists of scipy.sparse matrices (m x n, k x n), or
+        tuples (nz_offs, colptr, rowval, nzval) of host arrays."""
+        n, m, k = self.n, self.m, self.k
+        B = np.size(c) // n
+        _check_sizes(B, c=(c, B * n), b=(b if m else None, B * m), h=(h, B * k), sing=(sing, B))
+        Acsc = (A_mats if isinstance(A_mats, tuple) else _csc_arrays(A_mats, m, n, index_base)) if m else None
+        Gcsc = G_mats if isinstance(G_mats, tuple) else _csc_arrays(G_mats, k, n, index_base)
+        Acsc = [np.ascontiguousarray(a) for a in Acsc] if Acsc is not None else [None] * 4
+        Gcsc = [np.ascontiguousarray(a) for a in Gcsc]
+        t = C.c_int64()
+        P = self._params(maxit, tol, step, sigma_exp, init_eps)
+        p = _lib.ptr
+        _lib.check(_lib.load().socp_ingest_submit_csc(
+            self.handle, B, p(_host(c)), p(_host(b) if m else None), p(_host(h)),
+            p(None if sing is None else _host(sing, np.uint8)), *[p(a) for a in Acsc], *[p(a) for a in Gcsc],
+            index_base, P, C.byref(t)))
+        self._batch[t.value] = B
+        return t.value
+
+    def wait(self, ticket, res=False):
+        B = self._batch.pop(ticket, None)
+        if B is None:
+            raise ValueError(f"unknown ticket {ticket}")
+        n, m, k = self.n, self.m, self.k
+        out = dict(x=np.zeros(B * n), y=np.zeros(max(B * m, 1)), z=np.zeros(B * k), s=np.zeros(B * k),
+                   iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32))
+        if res:
+            out["res"] = np.zeros(3 * B)
+        p = _lib.ptr
+        _lib.check(_lib.load().socp_ingest_wait(self.handle, ticket, p(out["x"]), p(out["y"] if m else None),
+                                                p(out["z"]), p(out["s"]), p(out["iters"]), p(out["status"]),
+                                                p(out.get("res"))))
+        out["y"] = out["y"][:B * m]
+        return out
 
 
 def generate(cones, B, n, m, k, seed, first_problem=0, *, ctx=None, device=None):

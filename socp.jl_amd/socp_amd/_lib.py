@@ -29,6 +29,8 @@ EXPORTED = [
     "socp_comm_destroy", "socp_allgather_status", "socp_allgather_outcomes",
     "socp_dense_create", "socp_dense_setup_iter", "socp_dense_solve_kkt", "socp_dense_h2d_bytes",
     "socp_dense_record_bytes", "socp_dense_destroy",
+    "socp_ingest_create", "socp_ingest_next_inputs", "socp_ingest_submit", "socp_ingest_submit_csc",
+    "socp_ingest_wait", "socp_ingest_destroy",
 ]
 
 OUTCOME_BYTES = 32  # sizeof(socp_outcome): int32 status, int32 iters, double rd, rp, gap
@@ -110,6 +112,14 @@ def load():
         L.socp_dense_record_bytes.argtypes = [vp]
         L.socp_dense_record_bytes.restype = C.c_int64
         L.socp_dense_destroy.argtypes = [vp]
+    if hasattr(L, "socp_ingest_create"):  # pipelined ingest (absent from older A/B builds)
+        L.socp_ingest_create.argtypes = common + [C.c_int32, C.POINTER(C.c_void_p)]
+        L.socp_ingest_next_inputs.argtypes = [vp] + [C.POINTER(C.c_void_p)] * 6
+        L.socp_ingest_submit.argtypes = [vp, C.c_int64] + [dp] * 5 + [u8p, C.POINTER(Params), C.POINTER(C.c_int64)]
+        L.socp_ingest_submit_csc.argtypes = ([vp, C.c_int64] + [dp] * 3 + [u8p] + [vp] * 4 + [vp] * 4
+                                             + [C.c_int32, C.POINTER(Params), C.POINTER(C.c_int64)])
+        L.socp_ingest_wait.argtypes = [vp, C.c_int64] + [dp] * 4 + [i32p, i32p, dp]
+        L.socp_ingest_destroy.argtypes = [vp]
     if hasattr(L, "socp_comm_init"):  # RCCL gather (absent from libraries built before it)
         L.socp_comm_unique_id.argtypes = [vp]
         L.socp_comm_init.argtypes = [vp, C.c_int, C.c_int, vp, C.POINTER(C.c_void_p)]
