@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 import oracle as O  # noqa: E402
 from problems import kat_problem  # noqa: E402
-from socp_amd.configs import C0B, C1, C2  # noqa: E402
+from socp_amd.configs import C0B, C1, C2, C4  # noqa: E402
 
 
 def b64(a):
@@ -70,7 +70,9 @@ def main():
     for name in ("soc1", "soc2", "soc3"):
         cones, c, A, b, G, h = kat_problem(kats[name])
         out["cases"].append(case(name, cones, c, A, b, G, h, 12, {"kats": name}))
-    for cfg, count, iters in ((C0B, 4, 6), (C1, 8, 4), (C2, 4, 7)):
+    # C4 (n=512): its bench K=5 iterations, 4 problems (the
+    # blocked kernel's configuration)
+    for cfg, count, iters in ((C0B, 4, 6), (C1, 8, 4), (C2, 4, 7), (C4, 4, 5)):
         d = O.generate(cfg.cones, count, cfg.n, cfg.m, cfg.k, cfg.seed)
         for p in range(count):
             c = d["c"][p * cfg.n:(p + 1) * cfg.n]

@@ -57,6 +57,7 @@ def test_fixture_shape(fixture):
     names = [c["name"] for c in fixture["cases"]]
     assert {"soc1", "soc2", "soc3"} <= set(names)
     assert sum(n.startswith("C2#") for n in names) >= 4 and sum(n.startswith("C1#") for n in names) >= 8
+    assert sum(n.startswith("C4#") for n in names) >= 4
     for c in fixture["cases"]:
         for it in c["iterates"]:
             assert len(_arr(it["x"])) == c["n"] and len(_arr(it["z"])) == c["k"] and len(_arr(it["s"])) == c["k"]
@@ -64,6 +65,8 @@ def test_fixture_shape(fixture):
 
 def test_oracle_reproduces_fixture(fixture, kats, oracle):
     for case in fixture["cases"]:
+        if case["name"].startswith("C4#") and case["name"] != "C4#0":
+            continue  # ~11 s of oracle per C4 case: one keeps the CPU suite short
         cones, c, A, b, G, h = _problem(case, kats, oracle)
         T = len(case["iterates"]) - 1
         r = oracle.solve_trace(cones, c, A, b, G, h, params=oracle.Params(maxit=T, tol=0.0))

@@ -144,6 +144,40 @@ def test_c4_trajectory(oracle):
         assert_trajectory(cfg, g, r, B, 1e-8, K)
 
 
+def test_c4_trajectory_k1_to_k5_fixture():
+    """C4 at its bench K: the 4 committed oracle trajectories (tests/golden/
+    trajectories.json, cases C4#0..3) solved as one batch for K = 1..5.  kappa_2(H)
+    grows from ~1e3 to ~1e9 over these iterates (it passes 1e5 at the third or
+    fourth), so the gate scales with the worst conditioning met on the way:
+    rel <= max(1e-8, 1e-12 * max_j<=K kappa_2(H_j)) -- P4's 1e-8 while
+    kappa <= 1e4, u * kappa with a 1e4 margin after that."""
+    import base64
+    import json
+    import os
+    cfg = C4
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "trajectories.json")) as f:
+        cases = [c for c in json.load(f)["cases"] if c["name"].startswith("C4#")]
+    assert len(cases) >= 4
+    B = len(cases)
+    assert [c["source"]["problem"] for c in cases] == list(range(B))
+    c, A, b, G, h = (t.cpu().numpy() for t in S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cases[0]["source"]["seed"]))
+    sing = np.zeros(B, np.uint8)
+    arr = lambda s: np.frombuffer(base64.b64decode(s), dtype="<f8")  # noqa: E731
+    worst = []
+    for K in range(1, 6):
+        g = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=K, tol=0.0)
+        assert (g["status"] == S.MAXIT).all(), (K, g["status"])
+        for p, case in enumerate(cases):
+            kap = max(it["kappa_H"] for it in case["iterates"][:K])
+            tol = max(1e-8, 1e-12 * kap)
+            it = case["iterates"][K]
+            for key, L in (("x", cfg.n), ("z", cfg.k), ("s", cfg.k)):
+                e = rel(g[key][p * L:(p + 1) * L], arr(it[key]))
+                worst.append((e / tol, K, p, key, e, tol))
+                assert e <= tol, (K, p, key, e, tol)
+    print("worst error/tolerance ratios:", sorted(worst, reverse=True)[:3])
+
+
 def test_c4_full_batch_properties():
     """The BASELINE C4 batch (1,024 problems, fixed-K=5, device-resident): every
     problem runs its 5 iterations and stays strictly inside its 8 cones."""

@@ -1,0 +1,109 @@
+"""C2 under the reference's stopping rule (solver.jl:105,122: maxit 40,
+absolute tol 1e-5): the HIP outcome of the first 4,096 C2 problems against the
+oracle's (tests/golden/c2_refrule_outcomes.json, made by
+tests/golden/make_outcomes.py), in both operation orders the oracle has.
+
+Near the tolerance the iterates approach the cone boundary and whether a
+problem converges, stalls at maxit, loses positive definiteness of H (chol(H))
+or hits sqrt of a negative number (domain) is decided by rounding.  The
+reference's own operation order (dense iW*iW', scalings.jl:108) loses the most
+there; the structured order (X = W^-1 G, the order the HIP kernels and the
+oracle's F_STRUCTURED mode share) the least.  Measured on MI355X (4,096
+problems, [converged, maxit, chol(H), chol(S), domain]): reference order
+[1517, 805, 138, 0, 1636], structured [3337, 2, 652, 0, 105], HIP
+[3532, 3, 484, 0, 77].  Gates, set a few points inside those:
+  * vs the structured oracle: HIP converges on no fewer problems than it
+    minus 2 % of the batch and fails (chol/domain) on no more plus 2 %; the
+    same outcome on >= 82 % of problems (measured 86.4 %); of the problems it
+    converges on, HIP converges on >= 93 % (95.7 %); where both converge,
+    |d iters| <= 1 on >= 98 % (99.7 %);
+  * vs the reference-order oracle: of the problems it converges on, HIP
+    converges on >= 95 % (97.6 %) and the rest end at chol(H)/domain, not
+    maxit; HIP converges on at least as many problems overall; where both
+    converge, |d iters| <= 1 on >= 88 % (92.4 %);
+  * every HIP "converged" problem meets the exit test (rd + rp + gap < 1e-5).
+"""
+import base64
+import json
+import os
+
+import numpy as np
+import pytest
+
+import socp_amd as S
+from socp_amd.configs import C2
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _arr(s, dt):
+    return np.frombuffer(base64.b64decode(s), dtype=dt)
+
+
+@pytest.fixture(scope="module")
+def outcomes():
+    with open(os.path.join(HERE, "golden", "c2_refrule_outcomes.json")) as f:
+        fx = json.load(f)
+    cfg, B = C2, fx["batch"]
+    c, A, b, G, h = S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, fx["seed"])
+    import torch
+    sing = torch.zeros(B, dtype=torch.uint8, device=G.device)
+    g = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, h, sing, maxit=fx["maxit"], tol=fx["tol"],
+                      res=True)
+    torch.cuda.synchronize()
+    hip = dict(status=g["status"].cpu().numpy(), iters=g["iters"].cpu().numpy(),
+               res=g["res"].cpu().numpy().reshape(B, 3))
+    runs = {name: dict(status=_arr(r["status"], "<i1").astype(np.int32), iters=_arr(r["iters"], "<i1").astype(np.int32),
+                       res=_arr(r["res"], "<f8").reshape(B, 3))
+            for name, r in fx["runs"].items()}
+    hist = {name: np.bincount(r["status"], minlength=5) for name, r in runs.items()}
+    hist["hip"] = np.bincount(hip["status"], minlength=5)
+    print("\nC2 reference rule, 4096 problems [converged, maxit, chol(H), chol(S), domain]:")
+    for name, hh in hist.items():
+        print(f"  {name:16s} {hh.tolist()}")
+    for name, r in runs.items():
+        same = (hip["status"] == r["status"]).mean()
+        both = (hip["status"] == S.CONVERGED) & (r["status"] == S.CONVERGED)
+        di = np.abs(hip["iters"][both] - r["iters"][both])
+        rc = r["status"] == S.CONVERGED
+        print(f"  vs {name}: same outcome {same:.4f}; of its converged, HIP converged "
+              f"{(hip['status'][rc] == S.CONVERGED).mean():.4f} (HIP outcomes {np.bincount(hip['status'][rc], minlength=5).tolist()}); "
+              f"both converged {both.sum()}: |d iters| = 0: {(di == 0).mean():.3f}, <= 1: {(di <= 1).mean():.3f}, "
+              f"<= 2: {(di <= 2).mean():.3f}, max {di.max() if di.size else 0}")
+    return dict(B=B, hip=hip, runs=runs, hist=hist)
+
+
+def test_hip_exit_test_holds(outcomes):
+    hip = outcomes["hip"]
+    conv = hip["status"] == S.CONVERGED
+    assert conv.any()
+    assert (hip["res"][conv].sum(axis=1) < 1e-5).all()
+    assert (hip["iters"][conv] <= 40).all()
+
+
+def test_vs_structured_oracle(outcomes):
+    B, hip, r = outcomes["B"], outcomes["hip"], outcomes["runs"]["structured"]
+    hh, ho = outcomes["hist"]["hip"], outcomes["hist"]["structured"]
+    fail = lambda hst: hst[S.CHOL_H_FAILED] + hst[S.CHOL_S_FAILED] + hst[S.DOMAIN_ERROR]  # noqa: E731
+    assert hh[S.CONVERGED] >= ho[S.CONVERGED] - 0.02 * B, (hh.tolist(), ho.tolist())
+    assert fail(hh) <= fail(ho) + 0.02 * B, (hh.tolist(), ho.tolist())
+    assert (hip["status"] == r["status"]).mean() >= 0.82
+    rc = r["status"] == S.CONVERGED
+    assert (hip["status"][rc] == S.CONVERGED).mean() >= 0.93
+    both = (hip["status"] == S.CONVERGED) & rc
+    di = np.abs(hip["iters"][both] - r["iters"][both])
+    assert (di <= 1).mean() >= 0.98, np.bincount(di)
+
+
+def test_vs_reference_order_oracle(outcomes):
+    B, hip, r = outcomes["B"], outcomes["hip"], outcomes["runs"]["reference_order"]
+    rc = r["status"] == S.CONVERGED
+    hs = hip["status"][rc]
+    assert (hs == S.CONVERGED).mean() >= 0.95, np.bincount(hs, minlength=5)
+    assert (hs != S.MAXIT).all(), np.bincount(hs, minlength=5)
+    assert (hip["status"] == S.CONVERGED).sum() >= rc.sum()
+    both = (hip["status"] == S.CONVERGED) & rc
+    di = np.abs(hip["iters"][both] - r["iters"][both])
+    assert (di <= 1).mean() >= 0.88, np.bincount(di)
