@@ -241,7 +241,18 @@ static const char* kUnsupported =
 // ---------------------------------------------------------------- launch
 static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_DIAG builds)
 
+// 1, 2 or 4 when every cone is 16, 32 or 64 long (each cone is then whole
+// 16-lane rows of one 64-element slot), else 0
+static int cone_rows_uniform(const ConeTable& t, int nc) {
+  const int d = t.dim[0];
+  if (d != 16 && d != 32 && d != 64) return 0;
+  for (int c = 1; c < nc; ++c)
+    if (t.dim[c] != d) return 0;
+  return d / 16;
+}
+
 static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
+  args.al_rows = cone_rows_uniform(args.cones, args.nc);
   size_t lds = small_lds_bytes(v->NQ, v->NP, v->MQ);
   if (lds > 160 * 1024) return fail(SOCP_E_UNSUPPORTED, "LDS footprint too large");
   const bool solver = args.mode == MODE_SOLVE;

@@ -56,7 +56,8 @@ struct SmallArgs {
   int32_t n, m, k, nc;
   int32_t maxit, sigma_exp;
   double tol, step, init_eps;
-  int32_t flags, mode, deg, pad0;
+  int32_t flags, mode, deg;
+  int32_t al_rows;  // 1, 2 or 4 when every cone is 16, 32 or 64 long (so 16-lane-row aligned): register-only cone reductions; 0 otherwise
   const double *c, *A, *b, *G, *h;
   const uint8_t* sing;
   double *x, *y, *z, *s;
@@ -113,8 +114,13 @@ struct Shape {
   static constexpr int O_A = O_KV + NKV * KS;
   static constexpr int O_NV = O_A + MPAD * LDA;    // n-vectors: c x rd rx n0 tn
   static constexpr int O_MV = O_NV + 6 * NPAD;     // m-vectors: b y rp ry m0 tm
-  static constexpr int O_U = O_MV + 6 * MPAD;      // U[NCS][NPAD]
-  static constexpr int O_TB = O_U + NCS * NPAD;    // tile transpose [16][17]
+  // U[NCS][NPAD] (the SYRK's cone rows) and, for m <= 16, A Li (MPAD x LDA,
+  // from the Schur step to the solves): their lifetimes do not overlap
+  static constexpr bool AL_LDS = MQ == 1;
+  static constexpr int UAL = (AL_LDS && MPAD * LDA > NCS * NPAD) ? MPAD * LDA : NCS * NPAD;
+  static constexpr int O_U = O_MV + 6 * MPAD;
+  static constexpr int O_AL = O_U;
+  static constexpr int O_TB = O_U + UAL;           // tile transpose [16][17]
   static constexpr int TOTAL = O_TB + 16 * 17;
   static constexpr int nv(int id) { return O_NV + id * NPAD; }
   static constexpr int mv(int id) { return O_MV + id * MPAD; }
@@ -126,13 +132,15 @@ enum : int { MV_B, MV_Y, MV_RP, MV_RY, MV_M0, MV_TM };
 // tiles in lane order, LAM WB CA CBV IL, the per-cone constants, the sing flag
 inline int64_t small_rec_doubles(int NQ, int NP, int MQ) {
   const int64_t NT = NQ * (NQ + 1) / 2, MT = MQ * (MQ + 1) / 2;
-  return (NT + MT) * 256 + 5 * (int64_t)(4 * NP) + 20 * NCS + 8;
+  const int64_t al = MQ == 1 ? (int64_t)16 * (16 * NQ + 1) : 0;  // A Li kept in LDS (Shape::AL_LDS)
+  return (NT + MT) * 256 + 5 * (int64_t)(4 * NP) + 20 * NCS + al + 8;
 }
 
 inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
   int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = NPAD + 1;
   int KS = 4 * NP;  // Shape::KS
-  int total = O_KV + NKV * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + NCS * NPAD + 16 * 17;
+  int ual = (MQ == 1 && MPAD * LDA > NCS * NPAD) ? MPAD * LDA : NCS * NPAD;  // Shape::UAL
+  int total = O_KV + NKV * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + ual + 16 * 17;
   return (size_t)total * sizeof(double);
 }
 
@@ -140,7 +148,7 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
 // deltas accumulated per problem and added to a global table by lane 0.
 #ifdef SOCP_DIAG
 #define NSTAMP 12
-#define NSUBSTAMP 6  // sub-phases of the H sweep, slots NSTAMP+1 ..
+#define NSUBSTAMP 11  // sub-phases (0-3 the H sweep, 4-10 solve / cone-op parts), slots NSTAMP+1 ..
 // Totals live in LDS (lane 0 read-modify-writes them), so the stamps cost no
 // registers beyond the last timestamp; they are flushed once per wave.
 #define STAMP_DECL uint64_t st_last = 0;
@@ -149,11 +157,13 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
     if (threadIdx.x == 0) reinterpret_cast<unsigned long long*>(socp_lds + O_STAMPS)[i] += t_ - st_last; \
     st_last = t_; } while (0)
 #define STAMP_SUB(i) do { if constexpr (SUBST) STAMP(NSTAMP + 1 + (i)); } while (0)
+#define STAMP_X(i) STAMP(NSTAMP + 1 + (i))
 #else
 #define STAMP_DECL
 #define STAMP_START_S(obj) do {} while (0)
 #define STAMP(i) do {} while (0)
 #define STAMP_SUB(i) do {} while (0)
+#define STAMP_X(i) do {} while (0)
 #endif
 enum { SP_LOAD, SP_SCALING, SP_RESID, SP_U, SP_SYRK, SP_SWEEP_H, SP_SCHUR, SP_SOLVE, SP_STEP, SP_VOP,
        SP_STORE, SP_OTHER };
@@ -271,6 +281,33 @@ __device__ __forceinline__ double rows_sum(double x) {
   const auto c = __builtin_amdgcn_permlane16_swap(ylo, ylo, false, false);
   const auto d = __builtin_amdgcn_permlane16_swap(yhi, yhi, false, false);
   return __hiloint2double((int)d[0], (int)c[0]) + __hiloint2double((int)d[1], (int)c[1]);
+}
+
+// Cone reductions when every cone is R = 1, 2 or 4 whole 16-lane rows (all
+// cones 16, 32 or 64 long): all-reduce inside each row by DPP rotations, then
+// across the cone's rows with the row-swap permutes -- every lane of the cone
+// gets the total, no predicates, no LDS.  MX: max instead of sum.
+template <bool MX>
+__device__ __forceinline__ double rop(double a, double b) { return MX ? fmax(a, b) : a + b; }
+template <bool MX>
+__device__ __forceinline__ double cone_allreduce_rows(double v, int R) {
+  v = rop<MX>(v, dpp_all<0x128>(v));  // row_ror:8
+  v = rop<MX>(v, dpp_all<0x124>(v));  // row_ror:4
+  v = rop<MX>(v, dpp_all<0x122>(v));  // row_ror:2
+  v = rop<MX>(v, dpp_all<0x121>(v));  // row_ror:1
+  if (R >= 2) {  // rows (2r, 2r+1)
+    const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+    const auto c = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto d = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    v = rop<MX>(__hiloint2double((int)d[0], (int)c[0]), __hiloint2double((int)d[1], (int)c[1]));
+  }
+  if (R == 4) {  // halves (l, l ^ 32)
+    const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+    const auto c = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto d = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    v = rop<MX>(__hiloint2double((int)d[0], (int)c[0]), __hiloint2double((int)d[1], (int)c[1]));
+  }
+  return v;
 }
 
 // Butterfly partner inside a 16-lane row for reduce-scatter level M, by DPP:
@@ -395,7 +432,8 @@ struct Small {
   static constexpr int NT = NQ * (NQ + 1) / 2;
   static constexpr int MT = MQ * (MQ + 1) / 2;
   static constexpr int NPAD = SH::NPAD, KP = SH::KP, MPAD = SH::MPAD, LDA = SH::LDA;
-  static constexpr int O_A = SH::O_A, O_U = SH::O_U, O_TB = SH::O_TB;
+  static constexpr int O_A = SH::O_A, O_U = SH::O_U, O_AL = SH::O_AL, O_TB = SH::O_TB;
+  static constexpr bool AL_LDS = SH::AL_LDS;
   static constexpr int C_ = SH::nv(NV_C), X_ = SH::nv(NV_X), RD = SH::nv(NV_RD),
                        RX = SH::nv(NV_RX), N0 = SH::nv(NV_N0), TN = SH::nv(NV_TN);
   static constexpr int B_ = SH::mv(MV_B), Y_ = SH::mv(MV_Y), RP = SH::mv(MV_RP),
@@ -599,6 +637,15 @@ struct Small {
     MARK_BEGIN("cone_reduce");
     LANE_IDS();
     constexpr int NS = KP > 64 ? 2 : 1;  // slots that can hold elements of this shape
+    if (a.al_rows) {  // row-aligned cones: registers only
+      const int R = a.al_rows;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+          v[s][q] = ((MX >> q) & 1) ? cone_allreduce_rows<true>(v[s][q], R) : cone_allreduce_rows<false>(v[s][q], R);
+      return;
+    }
     const int rl = lane & 15;
 #define SOCP_SCAN_STEP(CTRL, OK)                                         \
   _Pragma("unroll") for (int s = 0; s < NS; ++s) {                       \
@@ -653,6 +700,13 @@ struct Small {
     LANE_IDS();
     constexpr int NS = KP > 64 ? 2 : 1;
     const int rl = lane & 15;
+    if (a.al_rows) {  // row-aligned cones: every lane of the cone gets its total
+      const int R = a.al_rows;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int q = 0; q < NV; ++q) v[s][q] = cone_allreduce_rows<false>(v[s][q], R);
+    } else {
 #define SOCP_SCAN_STEP(CTRL, OK)                         \
   _Pragma("unroll") for (int s = 0; s < NS; ++s) {       \
     const int st = ssl[s];                               \
@@ -669,6 +723,7 @@ struct Small {
     SOCP_SCAN_STEP(0x142, ((lane >> 4) & 1) && ((lane & ~15) - 1 >= st))
     SOCP_SCAN_STEP(0x143, lane >= 32 && 31 >= st)
 #undef SOCP_SCAN_STEP
+    }
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (lane == sle[s]) {
@@ -850,6 +905,7 @@ struct Small {
       v[s][2] = tail ? wb[s] * dz[s] : 0.0;
     }
     cone_reduce<3, 0>(v);
+    STAMP_X(8);
     MARK_BEGIN("head_post");
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -919,6 +975,7 @@ struct Small {
       v[s][2] = tail ? lam[s] * k0[s] : 0.0;
     }
     cone_reduce<3, 0>(v);
+    STAMP_X(9);
     MARK_BEGIN("tail_post1");
     double y[2], y0v[2], kn[2], kn0[2], ly[2], lkn[2];
 #pragma unroll
@@ -974,6 +1031,7 @@ struct Small {
       w[s][4] = real ? y[s] * kn[s] : 0.0;
     }
     cone_reduce<5, 0xC>(w);
+    STAMP_X(10);
     MARK_BEGIN("tail_post2");
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -1570,6 +1628,12 @@ struct Small {
       if constexpr (KEEP_AL) {
 #pragma unroll
         for (int ti = 0; ti < NQ; ++ti) AL[tq][ti] = transpose(ALc[ti]);  // A Li = (Li A')'
+      } else if constexpr (AL_LDS) {
+        // A Li row-major in LDS: lane (g, cl) holds (A Li)[16tq+cl][16ti+g+4r]
+#pragma unroll
+        for (int ti = 0; ti < NQ; ++ti)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) LDS(O_AL + (16 * tq + cl) * LDA + 16 * ti + g + 4 * r) = ALc[ti][r];
       }
     }
 #pragma unroll
@@ -1716,7 +1780,7 @@ struct Small {
   }
 
   // acc[q] (all lanes) = (A' v)[16q+cl]: rows split over the 4 lane groups
-  __device__ __forceinline__ void At_mv(int v, double (&acc)[NQ]) {
+  __device__ __forceinline__ void At_mv(int v, double (&acc)[NQ], int base = O_A) {
     MARK_BEGIN("At_mv");
     LANE_IDS();
 #pragma unroll
@@ -1726,7 +1790,7 @@ struct Small {
       const int i = g + 4 * s;
       const double vi = LDS(v + i);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc[q] = fma(LDS(O_A + i * LDA + 16 * q + cl), vi, acc[q]);
+      for (int q = 0; q < NQ; ++q) acc[q] = fma(LDS(base + i * LDA + 16 * q + cl), vi, acc[q]);
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -1804,15 +1868,28 @@ struct Small {
       }
     }
     SYNC();
+    STAMP_X(4);
     symv<NQ>(T, N0, TN);   // Li n0
+    STAMP_X(5);
     A_mv(TN, RP, M0);      // m0 = A Li n0 - dy
     SYNC();
     symv<MQ>(Sv, M0, RY);  // cy = S^-1 m0
     if (lane < m) LDS(M0 + lane) = (sing && !init) ? LDS(RP + lane) - LDS(RY + lane) : -LDS(RY + lane);
     SYNC();
+    STAMP_X(6);
     if constexpr (KEEP_AL) {
       // cx = Li (n0 + A'm0) = Li n0 + (A Li)' m0
       ALt_mv(M0, TN, RX);
+    } else if constexpr (AL_LDS) {
+      // cx = Li (n0 + A'm0) = Li n0 + (A Li)' m0: one Li product per solve
+      double at[NQ];
+      At_mv(M0, at, O_AL);
+      if (g == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) LDS(RX + 16 * q + cl) = LDS(TN + 16 * q + cl) + at[q];
+      }
+      SYNC();
+      STAMP_X(7);
     } else {
       double at[NQ];
       At_mv(M0, at);
@@ -1856,7 +1933,7 @@ struct Small {
   static __device__ constexpr int rec_kv(int v) {
     return v == 0 ? KV_LAM : v == 1 ? KV_WB : v == 2 ? KV_CA : v == 3 ? KV_CB : KV_IL;
   }
-  static constexpr int64_t REC_SING = (int64_t)(NT + MT) * 256 + 5 * KP + 20 * NCS;
+  static constexpr int64_t REC_SING = (int64_t)(NT + MT) * 256 + 5 * KP + 20 * NCS + (AL_LDS ? MPAD * LDA : 0);
   static constexpr int64_t REC_STATUS = REC_SING + 1;  // setup_iter's status, read first by solve_kkt
   __device__ __forceinline__ void store_record(int64_t p) {
     LANE_IDS();
@@ -1876,7 +1953,9 @@ struct Small {
       for (int i = lane; i < KP; i += 64) r[v * KP + i] = LDS(kvs(rec_kv(v)) + i);
     r += 5 * KP;
     for (int i = lane; i < 20 * NCS; i += 64) r[i] = LDS(O_CC + i);
-    if (lane == 0) r[20 * NCS] = sing ? 1.0 : 0.0;  // REC_SING
+    if constexpr (AL_LDS)
+      for (int i = lane; i < MPAD * LDA; i += 64) r[20 * NCS + i] = LDS(O_AL + i);
+    if (lane == 0) r[REC_SING - (NT + MT) * 256 - 5 * KP] = sing ? 1.0 : 0.0;  // REC_SING
   }
   __device__ __forceinline__ void load_record(int64_t p) {
     LANE_IDS();
@@ -1896,7 +1975,9 @@ struct Small {
       for (int i = lane; i < KP; i += 64) LDS(kvs(rec_kv(v)) + i) = r[v * KP + i];
     r += 5 * KP;
     for (int i = lane; i < 20 * NCS; i += 64) LDS(O_CC + i) = r[i];
-    sing = uni(r[20 * NCS]) != 0.0;
+    if constexpr (AL_LDS)
+      for (int i = lane; i < MPAD * LDA; i += 64) LDS(O_AL + i) = r[20 * NCS + i];
+    sing = uni(r[REC_SING - (NT + MT) * 256 - 5 * KP]) != 0.0;
     SYNC();
   }
 

@@ -25,11 +25,12 @@ for cname in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["C2", "C1"]):
     ctx.sync()
     v = buf.cpu().numpy().astype(float)
     iters = v[12]
-    tot = v[:12].sum() + v[13:19].sum()
+    tot = v[:12].sum() + v[13:24].sum()
     print(f"== {cname} B={B} K={K} kernel {ctx.last_kernel_ms():.2f} ms, iters {iters:.0f}, cycles/problem-iter {tot/iters:.0f}")
     for nm, x in zip(names, v[:12]):
         print(f"   {nm:8s} {x/iters:9.0f} cyc/it  {100*x/tot:5.1f}%")
-    subs = ["sw:fac0", "sw:fac+ops", "sw:T+Y", "sw:last", "sw:-", "sw:-"]
-    for nm, x in zip(subs, v[13:19]):
+    subs = ["sw:fac0", "sw:fac+ops", "sw:T+Y", "sw:last", "s:Gt", "s:symvH", "s:A,S", "s:ALt", "v:headred",
+            "v:tailred1", "v:tailred2"]
+    for nm, x in zip(subs, v[13:24]):
         if x:
             print(f"   {nm:9s} {x/iters:8.0f} cyc/it  {100*x/tot:5.1f}%")
