@@ -1799,7 +1799,7 @@ struct Small {
   }
   // out[i] = (A u)[i] - sub[i] for i < m (columns split over the 4 lane groups);
   // returns sum of out[i]^2 on lanes g == 0
-  __device__ __forceinline__ double A_mv(int u, int sub, int out) {
+  __device__ __forceinline__ double A_mv(int u, int sub, int out, int base = O_A) {
     MARK_BEGIN("A_mv");
     LANE_IDS();
     double sq = 0.0;
@@ -1808,7 +1808,7 @@ struct Small {
       const int i = 16 * tm + cl;
       double acc = 0.0;
 #pragma unroll
-      for (int t = 0; t < NQ * 4; ++t) acc = fma(LDS(O_A + i * LDA + g + 4 * t), LDS(u + g + 4 * t), acc);
+      for (int t = 0; t < NQ * 4; ++t) acc = fma(LDS(base + i * LDA + g + 4 * t), LDS(u + g + 4 * t), acc);
       acc = rows_sum(acc);
       if (g == 0 && i < m) {
         const double v = acc - LDS(sub + i);
@@ -1871,7 +1871,10 @@ struct Small {
     STAMP_X(4);
     symv<NQ>(T, N0, TN);   // Li n0
     STAMP_X(5);
-    A_mv(TN, RP, M0);      // m0 = A Li n0 - dy
+    if constexpr (AL_LDS)
+      A_mv(N0, RP, M0, O_AL);  // m0 = (A Li) n0 - dy: no wait for Li n0
+    else
+      A_mv(TN, RP, M0);        // m0 = A (Li n0) - dy
     SYNC();
     symv<MQ>(Sv, M0, RY);  // cy = S^-1 m0
     if (lane < m) LDS(M0 + lane) = (sing && !init) ? LDS(RP + lane) - LDS(RY + lane) : -LDS(RY + lane);
@@ -2162,14 +2165,13 @@ struct Small {
           STAMP(SP_OTHER);
           solve_head();
           STAMP(SP_VOP);
-          next = MP_SOLVE_MAT;
-          break;
+          [[fallthrough]];  // the three parts of a solve run back to back (a
+                            // trip through the phase dispatch costs ~1 % per transition)
         case MP_SOLVE_MAT:
           MARK_BEGIN("case MP_SOLVE_MAT");
           solve_matrix_part(ret == RET_INIT);
           STAMP(SP_SOLVE);
-          next = MP_SOLVE_TAIL;
-          break;
+          [[fallthrough]];
         case MP_SOLVE_TAIL: {
           MARK_BEGIN("case MP_SOLVE_TAIL");
           const bool do_step = ret == RET_AFFINE || ret == RET_COMBINED;
