@@ -2160,60 +2160,60 @@ struct Small {
           next = MP_FACTOR;
           break;
         }
-        case MP_SOLVE_HEAD:
-          MARK_BEGIN("case MP_SOLVE_HEAD");
-          STAMP(SP_OTHER);
-          solve_head();
-          STAMP(SP_VOP);
-          [[fallthrough]];  // the three parts of a solve run back to back (a
-                            // trip through the phase dispatch costs ~1 % per transition)
-        case MP_SOLVE_MAT:
-          MARK_BEGIN("case MP_SOLVE_MAT");
-          solve_matrix_part(ret == RET_INIT);
-          STAMP(SP_SOLVE);
-          [[fallthrough]];
-        case MP_SOLVE_TAIL: {
-          MARK_BEGIN("case MP_SOLVE_TAIL");
-          const bool do_step = ret == RET_AFFINE || ret == RET_COMBINED;
-          int dom = 0;
-          const double tstep = solve_tail(do_step, dm_aa, dom);
-          STAMP(SP_VOP);
-          if (ret == RET_KKT) {
-            status = 0;
-            for (int j = lane; j < n; j += 64) a.cx[p * n + j] = LDS(RX + j);
-            for (int i = lane; i < m; i += 64) a.cy[p * m + i] = LDS(RY + i);
-            for (int i = lane; i < k; i += 64) {
-              a.cz[p * k + i] = LDS(RZ + i);
-              a.cs[p * k + i] = LDS(RS + i);
+        case MP_SOLVE_HEAD: {
+          // a solve (densesolver.jl:54-90) -- head, matrix part, tail -- and,
+          // after the affine one, the combined one: without trips through the
+          // phase dispatch (each costs ~1 %)
+          for (;;) {
+            MARK_BEGIN("case MP_SOLVE_HEAD");
+            STAMP(SP_OTHER);
+            solve_head();
+            STAMP(SP_VOP);
+            MARK_BEGIN("case MP_SOLVE_MAT");
+            solve_matrix_part(ret == RET_INIT);
+            STAMP(SP_SOLVE);
+            MARK_BEGIN("case MP_SOLVE_TAIL");
+            const bool do_step = ret == RET_AFFINE || ret == RET_COMBINED;
+            int dom = 0;
+            const double tstep = solve_tail(do_step, dm_aa, dom);
+            STAMP(SP_VOP);
+            if (ret == RET_KKT) {
+              status = 0;
+              for (int j = lane; j < n; j += 64) a.cx[p * n + j] = LDS(RX + j);
+              for (int i = lane; i < m; i += 64) a.cy[p * m + i] = LDS(RY + i);
+              for (int i = lane; i < k; i += 64) {
+                a.cz[p * k + i] = LDS(RZ + i);
+                a.cs[p * k + i] = LDS(RS + i);
+              }
+              done = true;
+              break;
             }
-            done = true;
-            break;
-          }
-          if (ret == RET_INIT) {  // cone shift (solver.jl:86-104)
-            double alphp, alphd;  // max_step(-iz), max_step(iz)
-            maxstep_op(RZ, alphp, alphd);
-            for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(RX + j);
-            for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(RY + i);
-            for (int i = lane; i < k; i += 64) {
-              const double iz = LDS(RZ + i), e = e_of(i);
-              LDS(S_ + i) = (fabs(alphp) < a.init_eps) ? -iz : -iz + (1.0 + alphp) * e;
-              LDS(Z_ + i) = (fabs(alphd) < a.init_eps) ? iz : iz + (1.0 + alphd) * e;
+            if (ret == RET_INIT) {  // cone shift (solver.jl:86-104)
+              double alphp, alphd;  // max_step(-iz), max_step(iz)
+              maxstep_op(RZ, alphp, alphd);
+              for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(RX + j);
+              for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(RY + i);
+              for (int i = lane; i < k; i += 64) {
+                const double iz = LDS(RZ + i), e = e_of(i);
+                LDS(S_ + i) = (fabs(alphp) < a.init_eps) ? -iz : -iz + (1.0 + alphp) * e;
+                LDS(Z_ + i) = (fabs(alphd) < a.init_eps) ? iz : iz + (1.0 + alphd) * e;
+              }
+              SYNC();
+              next = MP_ITER;
+              break;
             }
-            SYNC();
-            next = MP_ITER;
-            break;
-          }
-          if (dom) {
-            status = ST_DOMAIN;
-            done = true;
-            break;
-          }
-          if (ret == RET_AFFINE) {  // centering + corrector, then the combined solve
-            affine_post(tstep, ll);
-            STAMP(SP_STEP);
-            ret = RET_COMBINED;
-            next = MP_SOLVE_HEAD;
-          } else {  // combined direction: step and update (solver.jl:143-150)
+            if (dom) {
+              status = ST_DOMAIN;
+              done = true;
+              break;
+            }
+            if (ret == RET_AFFINE) {  // centering + corrector, then the combined solve
+              affine_post(tstep, ll);
+              STAMP(SP_STEP);
+              ret = RET_COMBINED;
+              continue;
+            }
+            // combined direction: step and update (solver.jl:143-150)
             const double stp = tstep * a.step;
             for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(X_ + j) + LDS(RX + j) * stp;
             for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(Y_ + i) + LDS(RY + i) * stp;
@@ -2225,6 +2225,7 @@ struct Small {
             STAMP(SP_STEP);
             iters = ++it;
             next = MP_ITER;
+            break;
           }
           break;
         }
