@@ -350,7 +350,7 @@ def main():
         }
         if world == 1 and not args.no_ingest:
             line["ingest"] = ingest_line(S, cfg, B, K, tol, (c, A, b, G, h), args.steps, ctx)
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol)
             line["cpu_baseline_structured"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol,
                                                            structured=True)
