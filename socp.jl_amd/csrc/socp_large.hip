@@ -239,7 +239,7 @@ struct Large {
         }
       LV(L.o_rc + i) = (double)code;
     }
-    if (tid < 16) LV(L.o_red + 16 + tid) = 0.0;  // all-zero bits: the u64 stamp totals start at 0
+    if (tid < 32) LV(L.o_red + 16 + tid) = 0.0;  // all-zero bits: the u64 stamp totals start at 0
     BAR();
     st_last = __builtin_amdgcn_s_memtime();
   }
@@ -248,7 +248,7 @@ struct Large {
     BAR();
     if (tid == 0 && a.stamps) {
       const unsigned long long* st = reinterpret_cast<const unsigned long long*>(lg_lds + L.o_red + 16);
-      for (int i = 0; i <= NSTAMP; ++i) atomicAdd(a.stamps + i, st[i]);
+      for (int i = 0; i <= NSTAMP + NSUBSTAMP; ++i) atomicAdd(a.stamps + i, st[i]);
     }
 #endif
   }
@@ -919,6 +919,7 @@ struct Large {
         }
       }
       BAR();
+      LSTAMP(NSTAMP + 1 + 0);
       double Z[8][nb];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -988,6 +989,7 @@ struct Large {
         }
       }
       BAR();  // Yp and the pivot reciprocals complete
+      LSTAMP(NSTAMP + 1 + 1);
       if (!ok) return false;
       {
         // addresses recomputed from a fresh lane id: reusing the load's would
@@ -1004,6 +1006,7 @@ struct Large {
         }
       }
       BAR();  // panel P written back before the next catch-up reads its neighbours
+      LSTAMP(NSTAMP + 1 + 2);
     }
     // Final catch-up: block (I, J), I >= J, has seen the panels up to I; it
     // receives those after I.  Each block is thus read and written 3 times per
@@ -1028,6 +1031,7 @@ struct Large {
       }
     }
     BAR();
+    LSTAMP(NSTAMP + 1 + 3);
     return true;
   }
 
@@ -1086,7 +1090,9 @@ struct Large {
     LSTAMP(SP_SYRK);
     if (!sweep(Hm, L.NPAD)) return ST_CHOL_H;
     if (h_only) return 0;
+    LSTAMP(SP_SWEEP_H);
     finalize_sym(Hm, L.NPAD);
+    LSTAMP(NSTAMP + 1 + 4);
     LSTAMP(SP_SWEEP_H);
     const int NB = L.NPAD / 64, MB = L.MPAD / 64;
     for (int t = wv; t < NB * MB; t += NW) {
@@ -1106,6 +1112,7 @@ struct Large {
       store_blk(acc, Sm, L.MPAD, 64 * I, 64 * J, m);
     }
     BAR();
+    LSTAMP(SP_SCHUR);
     if (!sweep(Sm, L.MPAD)) return ST_CHOL_S;
     finalize_sym(Sm, L.MPAD);
     LSTAMP(SP_SCHUR);
@@ -1115,6 +1122,7 @@ struct Large {
   // ------------------------------------------------------------ mat-vecs
   // out[j] = (G' vin)[j] (+ add[j]) for j < n: a wavefront takes CG columns
   __device__ void gemv_Gt(int vin, int vout, int vadd) {
+    LSTAMP(SP_SOLVE);
     for (int j0 = CG * wv; j0 < n; j0 += CG * NW) {
       gcdbl* g0 = Gp + (int64_t)j0 * k;
       const int nl = n - j0;  // live columns u < nl (dead ones re-read column j0)
@@ -1133,9 +1141,11 @@ struct Large {
       }
     }
     BAR();
+    LSTAMP(NSTAMP + 1 + 5);
   }
   // out[i] = (G u)[i] (+ add[i]) - sub[i] for i < k: one thread per row
   __device__ void gemv_G(int u, int add, int sub, int out) {
+    LSTAMP(SP_SOLVE);
     for (int i = tid; i < k; i += NTH) {
       double acc = 0.0;
 #pragma unroll 16
@@ -1144,6 +1154,7 @@ struct Large {
       LV(out + i) = acc - LV(sub + i);
     }
     BAR();
+    LSTAMP(NSTAMP + 1 + 7);
   }
   // (A' v)[j] for one j (thread per column; At rows are contiguous in j)
   __device__ __forceinline__ double At_dot(int v, int j) const {
@@ -1173,6 +1184,7 @@ struct Large {
   }
   // out = M vin for a full symmetric column-major M (thread per row)
   __device__ void symv(gcdbl* M, int ld, int vin, int vout) {
+    LSTAMP(SP_SOLVE);
     for (int i = tid; i < ld; i += NTH) {
       double acc = 0.0;
 #pragma unroll 16
@@ -1180,6 +1192,7 @@ struct Large {
       LV(vout + i) = acc;
     }
     BAR();
+    LSTAMP(NSTAMP + 1 + 6);
   }
 
   // rd = A'y + G'z + c, rp = Ax - b, rz = Gx + s - h (solver.jl:109-118)

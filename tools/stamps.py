@@ -29,7 +29,10 @@ for cname in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["C2", "C1"]):
     print(f"== {cname} B={B} K={K} kernel {ctx.last_kernel_ms():.2f} ms, iters {iters:.0f}, cycles/problem-iter {tot/iters:.0f}")
     for nm, x in zip(names, v[:12]):
         print(f"   {nm:8s} {x/iters:9.0f} cyc/it  {100*x/tot:5.1f}%")
-    subs = ["sw:fac0", "sw:fac+ops", "sw:T+Y", "sw:last", "s:Gt", "s:symvH", "s:A,S", "s:ALt", "v:headred",
+    if cname == "C4":
+        subs = ["sw:catchup", "sw:pivots", "sw:writebk", "sw:final", "finalize", "gemv_Gt", "symv", "gemv_G"]
+    else:
+        subs = ["sw:fac0", "sw:fac+ops", "sw:T+Y", "sw:last", "s:Gt", "s:symvH", "s:A,S", "s:ALt", "v:headred",
             "v:tailred1", "v:tailred2"]
     for nm, x in zip(subs, v[13:24]):
         if x:
