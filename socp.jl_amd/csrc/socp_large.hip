@@ -52,6 +52,12 @@ extern __shared__ double lg_lds[];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
     __syncthreads();                                \
   } while (0)
+// LDS-only barrier: the global stores in flight stay in flight (a
+// __syncthreads would drain them first, one store round trip per barrier)
+#define LDS_BAR()                                                 \
+  do {                                                            \
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+  } while (0)
 
 // Diagnostic build (-DSOCP_DIAG): thread 0 adds per-phase s_memtime deltas
 // into u64 totals at LDS o_red + 16 (its own timeline: the phases end in
@@ -946,7 +952,7 @@ struct Large {
             }
           }
         }
-        __syncthreads();
+        LDS_BAR();  // the pivot row's Yp / rv stores drain by the panel's BAR()
         const double d = LV(buf + P0 + c);
         ok = ok && (d > 0.0);
         const double r = 1.0 / d;
@@ -1215,7 +1221,7 @@ struct Large {
 
   // The matrix part of solve_kkt (densesolver.jl:66-85): n0 = GWiWi*k2 + dx
   // (+A'dy if sing); m0 = A Li n0 - dy; cy = S^-1 m0; m0 = sing ? dy - cy : -cy
-  // (init: -cy); n0 += A'm0; cx = Li n0; k1 = G cx - k2.
+  // (init: -cy); cx = Li (n0 + A'm0), taken as Li n0 + (Li A') m0; k1 = G cx - k2.
   // In: RD RP T2 K2.  Out: RX RY K1.
   __device__ void solve_matrix_part(bool init) {
     gemv_Gt(T2, N0, RD);
@@ -1228,9 +1234,14 @@ struct Large {
     symv(Sm, L.MPAD, M0, RY);
     for (int r = tid; r < m; r += NTH) LV(M0 + r) = (sing && !init) ? LV(RP + r) - LV(RY + r) : -LV(RY + r);
     BAR();
-    for (int j = tid; j < n; j += NTH) LV(N0 + j) = LV(N0 + j) + At_dot(M0, j);
+    // cx = Li (n0 + A'm0) = Li n0 + (Li A') m0: one pass over Li per solve
+    // (T = Li A' is the factor's, column-major NPAD x MPAD)
+    for (int j = tid; j < n; j += NTH) {
+      double acc = 0.0;
+      for (int r = 0; r < m; ++r) acc = fma(Tm[(int64_t)r * L.NPAD + j], LV(M0 + r), acc);
+      LV(RX + j) = LV(TN + j) + acc;
+    }
     BAR();
-    symv(Hm, L.NPAD, N0, RX);
     gemv_G(RX, -1, K2, K1);
   }
 
