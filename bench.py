@@ -203,6 +203,122 @@ def ingest_line(S, cfg, B, K, tol, dev_data, steps, ctx):
     }
 
 
+def sqr_model(n, m, k, cones):
+    """Algorithmic flops and bytes of one rank-update KKT iteration per problem
+    (setup_iter + 2 x solve_kkt of spsolver.jl:60-130): setup = G'DG (one
+    triangle) + chol(H) + per SOC cone G'u, G'v and two rank-1 modifications
+    + L^-1 A' + S + chol(S); solve = G'v, Gv, two H and one S triangular pair,
+    A/A' mat-vecs.  Bytes: setup reads G, A, s, z and writes the record
+    (L_H, L_S, lambda, wb); each solve reads G, A, the record and 2(n+m+2k)
+    vector entries."""
+    soc = [(o, d) for kind, o, d in cones if kind == 1]
+    f_setup = (n * (n + 1) * k + n ** 3 / 3.0 + sum(4 * d * n + 4 * n * n for _, d in soc)
+               + m * n * n + m * (m + 1) * n + m ** 3 / 3.0 + 20 * k)
+    f_solve = 4 * k * n + 4 * n * n + 2 * m * m + 4 * m * n + 30 * k
+    rec = n * n + m * m + 2 * k
+    b_setup = 8 * (k * n + m * n + 2 * k + rec)
+    b_solve = 8 * (k * n + m * n + rec + 2 * (n + m + 2 * k))
+    return f_setup, f_solve, b_setup, b_solve
+
+
+def sqr_bench(args):
+    """--mode sqr: the rank-update plugin (socp_sqr_*, SparseSolver + SqrScaling,
+    spsolver.jl / sqrscalings.jl) at the config's shape.  A step = setup_iter +
+    two solve_kkt (one IPM iteration's KKT work) over the whole batch, device
+    tensors, at the interior iterate the dense solver reaches after 3
+    iterations.  HBM-bound by the algorithmic model (sqr_model)."""
+    import torch
+    import socp_amd as S
+    from socp_amd.configs import CONFIGS
+    cfg = CONFIGS[args.config]
+    B = args.batch or cfg.batch
+    n, m, k = cfg.n, cfg.m, cfg.k
+    ctx = S.Context(0)
+    c, A, b, G, h = S.generate(cfg.cones, B, n, m, k, cfg.seed, ctx=ctx)
+    sing = torch.zeros(B, dtype=torch.uint8, device=G.device)
+    it = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=3, tol=0.0, ctx=ctx)
+    ctx.sync()
+    hd = S.SqrHandle(cfg.cones, n, m, k, A, G, sing, ctx=ctx)
+    gen = torch.Generator(device=G.device).manual_seed(5)
+    r = [torch.randn(B * q, dtype=torch.float64, device=G.device, generator=gen) for q in (n, m, k, k)]
+    out = None
+    t_setup, t_solve = [], []
+
+    def step(timed):
+        nonlocal out
+        hd.setup_iter(it["s"], it["z"])
+        if timed:
+            t_setup.append(ctx.last_kernel_ms())
+        for _ in range(2):
+            out = hd.solve_kkt(*r, out=out)
+            if timed:
+                t_solve.append(ctx.last_kernel_ms())
+
+    for _ in range(args.warmup):
+        step(False)
+    ctx.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(False)
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    for _ in range(2):
+        step(True)  # per-kernel HIP-event durations, outside the timed region
+    ms_setup = sum(t_setup) / len(t_setup)
+    ms_solve = sum(t_solve) / len(t_solve)
+    st = torch.bincount(out["status"].long(), minlength=5).tolist()
+    fs, fv, bs, bv = sqr_model(n, m, k, cfg.cones)
+    setup_gbs = bs * B / (ms_setup * 1e-3) / 1e9
+    solve_gbs = bv * B / (ms_solve * 1e-3) / 1e9
+    dominant = "setup" if ms_setup >= 2 * ms_solve else "solve"
+    ach = setup_gbs if dominant == "setup" else solve_gbs
+    line = {
+        "metric": "rank-update KKT plugin (SparseSolver + SqrScaling): setup_iter + 2 solve_kkt per problem",
+        "value": B * args.steps / dt,
+        "unit": "problem-iterations/s (KKT work of one IPM iteration)",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (device generator), iterates after 3 dense IPM iterations",
+        "config": {"workload": f"{cfg.name} shape: {B} problems, n={n}, m={m}, k={k}, cones {cone_str(cfg.cones)}; "
+                               "socp_sqr_setup_iter + 2 x socp_sqr_solve_kkt on device tensors",
+                   "global_batch": B, "parallelism": "dp1"},
+        "kernels": {"socp_sqr_setup_kernel_ms": ms_setup, "socp_sqr_solve_kernel_ms": ms_solve},
+        "status_counts": st,
+        "roofline": {"bound": "hbm", "kernel": f"socp_sqr_{dominant}_kernel", "achieved": ach,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                     "setup_GBps": setup_gbs, "solve_GBps": solve_gbs,
+                     "setup_TFLOPs": fs * B / (ms_setup * 1e-3) / 1e12,
+                     "solve_TFLOPs": fv * B / (ms_solve * 1e-3) / 1e12,
+                     "bytes_per_problem": {"setup": bs, "solve": bv}, "flops_per_problem": {"setup": fs, "solve": fv}},
+    }
+    if not args.no_cpu:
+        sys.path.insert(0, os.path.join(HERE, "oracle"))
+        import oracle as O  # test infrastructure: the CPU line only
+        import numpy as np
+        thr = baseline_threads()
+        chunk = 64 * thr
+        d = O.generate(cfg.cones, chunk, n, m, k, cfg.seed)
+        P = O.Params(maxit=cfg.fixed_k, tol=0.0, flags=O.F_SQR)
+        rates = []
+        for rep in range(4):
+            t1 = time.perf_counter()
+            rr = O.batch_solve(cfg.cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                               sing=np.zeros(chunk, np.uint8), params=P, nthreads=thr)
+            if rep:
+                rates.append(int(rr["iters"].sum()) / (time.perf_counter() - t1))
+        rates.sort()
+        info = host_cpu_info()
+        line["cpu_baseline"] = {"value": rates[len(rates) // 2], "unit": "problem-iterations/s (whole IPM iteration)",
+                                "cores": thr, "kind": "port", "cpu_model": info["model"], "nproc": info["nproc"],
+                                "sample": f"median of 3 reps x {chunk} {cfg.name} problems, fixed-K={cfg.fixed_k}, "
+                                          "oracle F_SQR (SqrScaling + rank-update factor restated, whole IPM "
+                                          "iteration: a superset of the KKT work timed on the GPU)"}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -211,9 +327,10 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--batch", type=int, default=0, help="problems per GPU (default: config batch)")
     ap.add_argument("--fixed-k", type=int, default=0)
-    ap.add_argument("--mode", choices=["fixed", "reference"], default="fixed",
+    ap.add_argument("--mode", choices=["fixed", "reference", "sqr"], default="fixed",
                     help="fixed: tol=0, K iterations (headline, SURVEY.md §8(d)(i)); reference: the "
-                         "reference's stopping rule, tol=1e-5 absolute, maxit=40, per-problem masking (§8(d)(ii))")
+                         "reference's stopping rule, tol=1e-5 absolute, maxit=40, per-problem masking (§8(d)(ii)); "
+                         "sqr: the rank-update KKT plugin (socp_sqr_*, spsolver.jl) at the config's shape")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="per CPU line (two lines)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ingest", action="store_true",
@@ -221,6 +338,8 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default: the newest profiles/rNN_pmc_traffic[_<config>].json")
     args = ap.parse_args()
+    if args.mode == "sqr":
+        return sqr_bench(args)
 
     import torch
     import torch.distributed as dist

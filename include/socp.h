@@ -204,6 +204,46 @@ int socp_dense_h2d_bytes(const socp_dense* h, int64_t* bytes);
 int64_t socp_dense_record_bytes(const socp_dense* h);
 int socp_dense_destroy(socp_dense* h);
 
+/* The rank-update plugin: SparseSolver with SqrScaling (spsolver.jl:1-130,
+ * sqrscalings.jl:8-214), the solver the reference's own tests and MOI run.
+ *   socp_sqr_create      replaces SparseSolver(pr) (spsolver.jl:24-57): A, G
+ *                        (and sing) copied into the handle once;
+ *   socp_sqr_setup_iter  replaces compute_scaling(cones, ::SqrScaling, s, z)
+ *                        (sqrscalings.jl:177-185) + setup_iter(::SparseSolver)
+ *                        (spsolver.jl:60-84): W^-2 = D + uu' - vv' per SOC cone,
+ *                        L L' = G'DG (+A'A when sing), one rank-1 update with
+ *                        G'u and one downdate with G'v per SOC cone
+ *                        (modify_factors!, sqrscalings.jl:160-194), and the
+ *                        factor of S = (L^-1 A')'(L^-1 A'); status[p] as for
+ *                        socp_dense_setup_iter (a downdate that loses positive
+ *                        definiteness is SOCP_CHOL_H_FAILED);
+ *   socp_sqr_solve_kkt   replaces solve_kkt(::SparseSolver) (spsolver.jl:86-130)
+ *                        by triangular solves against the record;
+ *   socp_sqr_factor      problem p's factor L of H after the modifications
+ *                        (n x n, column-major, zeros above the diagonal): the
+ *                        Gfact CHOLMOD factor of spsolver.jl:13 as a dense matrix;
+ *   socp_sqr_scaling     the SqrScaling fields l, wbs, mu (B x k, B x k,
+ *                        B x ncones) of the last setup_iter.
+ * CHOLMOD's fill-reducing permutation and supernodal LDL' are replaced by a
+ * dense factor: results agree with the reference to rounding, not bitwise.
+ * Shapes: n, m <= 64, k <= 256, <= 64 cones (socp_sqr_supported).  Flags and
+ * host/device pointer semantics as socp_dense_*. */
+typedef struct socp_sqr socp_sqr;
+int socp_sqr_supported(const socp_dims* dims);
+int socp_sqr_create(socp_ctx* ctx, const socp_dims* dims,
+                    const int32_t* cone_kind, const int32_t* cone_offs, const int32_t* cone_dim,
+                    const double* A, const double* G, const uint8_t* sing, int32_t flags,
+                    socp_sqr** out);
+int socp_sqr_setup_iter(socp_sqr* h, const double* s, const double* z, int32_t* status);
+int socp_sqr_solve_kkt(socp_sqr* h, const double* dx, const double* dy, const double* dz,
+                       const double* ds, double* cx, double* cy, double* cz, double* cs,
+                       int32_t* status);
+int socp_sqr_factor(socp_sqr* h, int64_t problem, double* L);
+int socp_sqr_scaling(socp_sqr* h, double* l, double* wbs, double* mu);
+int socp_sqr_h2d_bytes(const socp_sqr* h, int64_t* bytes);
+int64_t socp_sqr_record_bytes(const socp_sqr* h);
+int socp_sqr_destroy(socp_sqr* h);
+
 /* Device-side deterministic generator of feasible synthetic problems
  * (SURVEY.md §8(d)): counter-based SplitMix64 keyed on the GLOBAL problem
  * index first_problem + p, so shards of a multi-GPU run reproduce the same

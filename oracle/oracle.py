@@ -47,6 +47,7 @@ class Params(C.Structure):
 
 F_WARM_START = 2
 F_STRUCTURED = 16  # oracle-only: the build's structured algorithm (CPU baseline line)
+F_SQR = 32  # oracle-only: SqrScaling + SparseSolver (spsolver.jl, the rank-update path)
 
 
 def build(force: bool = False) -> str:
@@ -81,6 +82,8 @@ def lib():
         L.or_scale.argtypes = cones + [_dp, _dp, _dp, _dp, C.c_int]
         L.or_kkt_single.argtypes = cones + [C.c_int] * 3 + [_dp, _dp, C.c_int] + [_dp] * 6 + [_dp] * 4 + [C.c_void_p, C.c_void_p]
         L.or_kkt_single.restype = C.c_int
+        L.or_sqr_kkt_single.argtypes = cones + [C.c_int] * 3 + [_dp, _dp, C.c_int] + [_dp] * 6 + [_dp] * 4 + [C.c_void_p] * 4
+        L.or_sqr_kkt_single.restype = C.c_int
         L.or_batch_solve.argtypes = [C.c_int64, C.c_int, C.c_int, C.c_int] + cones + [_dp] * 5 + [C.c_void_p, C.POINTER(Params)] + [_dp] * 4 + [_ip, _ip, C.c_void_p, C.c_int]
         L.or_batch_solve.restype = C.c_int
         L.or_solve_trace.argtypes = [C.c_int] * 3 + cones + [_dp] * 5 + [C.c_int, C.POINTER(Params)] + [_dp] * 4 + [C.POINTER(C.c_int32), C.POINTER(C.c_int32), _dp, _dp, C.c_int]
@@ -176,6 +179,22 @@ def kkt_single(cones, A, G, sing, s, z, dx, dy, dz, ds, want_H=False):
         out["H"] = H.reshape(n, n, order="F")
         out["Li"] = Li.reshape(n, n, order="F")
     return out
+
+
+def sqr_kkt_single(cones, A, G, sing, s, z, dx, dy, dz, ds):
+    """SqrScaling + setup_iter + solve_kkt of the rank-update path (sqrscalings.jl:66-194,
+    spsolver.jl:60-130) at iterate (s,z).  Returns dict(cx,cy,cz,cs,status,L,l,wbs,mu);
+    L is the lower factor of H after modify_factors! (L L' = G'W^-2 G (+A'A))."""
+    A = np.asarray(A, dtype=np.float64).reshape(-1, G.shape[1]) if np.size(A) else np.zeros((0, G.shape[1]))
+    m, n = A.shape
+    k = G.shape[0]
+    cx, cy, cz, cs = np.zeros(n), np.zeros(m), np.zeros(k), np.zeros(k)
+    Lf, l, wbs, mu = np.zeros(n * n), np.zeros(k), np.zeros(k), np.zeros(len(cones))
+    st = lib().or_sqr_kkt_single(*cone_arrays(cones), n, m, k, _f(A.ravel(order="F")) if m else np.zeros(1),
+                                 _f(G.ravel(order="F")), int(sing), _f(s), _f(z), _f(dx),
+                                 _f(dy) if m else np.zeros(1), _f(dz), _f(ds), cx, cy if m else np.zeros(1), cz, cs,
+                                 Lf.ctypes.data, l.ctypes.data, wbs.ctypes.data, mu.ctypes.data)
+    return dict(cx=cx, cy=cy, cz=cz, cs=cs, status=st, L=Lf.reshape(n, n, order="F"), l=l, wbs=wbs, mu=mu)
 
 
 def sing_flag(G):

@@ -519,11 +519,249 @@ static void solve_kkt(dense_t* D, const cones_t* C, const scaling_t* S, const do
   scale_w(C, S, D->k0, cs);
 }
 
+/* ---------------- sqrscalings.jl + spsolver.jl (the rank-update path) ----------------
+ *
+ * SqrScaling (sqrscalings.jl:8-139): W^-2 = D + u u' - v v' per SOC cone, D
+ * diagonal.  SparseSolver (spsolver.jl:60-130): H = G'DG (+A'A if sing) is
+ * factored, then one rank-1 update with G'u and one downdate with G'v per SOC
+ * cone (modify_factors!, sqrscalings.jl:160-194), S = (L^-1 A')'(L^-1 A') is
+ * factored, and solve_kkt applies H^-1 and S^-1 by triangular solves.
+ *
+ * The reference runs this through CHOLMOD (SuiteSparse, the Julia stdlib's
+ * SuiteSparse.CHOLMOD: a fill-reducing permutation P, supernodal LDL'/LL',
+ * lowrankupdowndate! = the Davis-Hager rank-1 modification).  CHOLMOD is not
+ * part of /root/reference; restated here as the textbook algorithms on the
+ * dense lower factor, without the permutation: the factor of P H P' and H
+ * give the same solves to rounding.  A rank-1 update computes, column by
+ * column, r = sqrt(L_jj^2 + sig w_j^2), c = r / L_jj, s = w_j / L_jj,
+ * L_ij = (L_ij + sig s w_i) / c, w_i = c w_i - s L_ij (i > j); a downdate with
+ * r^2 <= 0 is a loss of positive definiteness -> status 2, as cholesky! of H.
+ * Pinned by runtests.jl:50-93 (the factor after modify_factors! inverts to the
+ * dense H^-1) and :95-128 (the KKT golden, produced on this path). */
+
+typedef struct {
+  double *D, *iWd, *u, *v; /* k each: diag of iWiW and iW; u, v of every SOC cone (disjoint supports) */
+} sqr_t;
+
+/* compute_scaling(::SqrScaling) (sqrscalings.jl:50-58 POC, :66-139 SOC), op order kept */
+static void sqr_compute_scaling(const cones_t* C, scaling_t* S, sqr_t* Q, const double* s,
+                                const double* z, int* dom) {
+  for (int c = 0; c < C->ncones; ++c) {
+    int o = C->offs[c], dim = C->dim[c];
+    if (C->kind[c] == POC) {
+      for (int ii = o; ii < o + dim; ++ii) {
+        Q->D[ii] = z[ii] / s[ii];
+        Q->iWd[ii] = jsqrt(z[ii] / s[ii], dom);
+        S->l[ii] = jsqrt(s[ii] * z[ii], dom);
+        S->wbs[ii] = jsqrt(s[ii] / z[ii], dom);
+        Q->u[ii] = 0.0;
+        Q->v[ii] = 0.0;
+      }
+      continue;
+    }
+    double *sbk = S->sik, *zbk = S->zik;
+    for (int i = 0; i < dim; ++i) {
+      sbk[i] = s[o + i];
+      zbk[i] = z[o + i];
+    }
+    double sprod = sbk[0] * sbk[0], zprod = zbk[0] * zbk[0];
+    for (int i = 1; i < dim; ++i) sprod -= sbk[i] * sbk[i];
+    for (int i = 1; i < dim; ++i) zprod -= zbk[i] * zbk[i];
+    double fs = 1.0 / jsqrt(sprod, dom), fz = 1.0 / jsqrt(zprod, dom);
+    for (int i = 0; i < dim; ++i) sbk[i] *= fs;
+    for (int i = 0; i < dim; ++i) zbk[i] *= fz;
+    double nsum = 0.0;
+    for (int i = 0; i < dim; ++i) nsum += zbk[i] * sbk[i];
+    double gamma = jsqrt((1.0 + nsum) / 2.0, dom);
+    double* wb = S->wbs + o;
+    wb[0] = (sbk[0] + zbk[0]) / (2.0 * gamma);
+    for (int i = 1; i < dim; ++i) wb[i] = (sbk[i] - zbk[i]) / (2.0 * gamma);
+    S->mu[c] = jsqrt(jsqrt(sprod / zprod, dom), dom);
+    double inusq = 1.0 / jsqrt(sprod / zprod, dom);
+    double inu = 1.0 / jsqrt(jsqrt(sprod / zprod, dom), dom);
+    double wb0 = wb[0], wb1sq = 0.0;
+    for (int i = 1; i < dim; ++i) wb1sq += wb[i] * wb[i];
+    double cv = -(1.0 + wb0 + wb1sq / (1.0 + wb0));
+    double d = 1.0 + 2.0 / (1.0 + wb0) + wb1sq / ((1.0 + wb0) * (1.0 + wb0));
+    double a = (wb0 * wb0 + wb1sq - cv * cv * wb1sq / (1.0 + d * wb1sq)) / 2.0;
+    double u0 = jsqrt(wb0 * wb0 + wb1sq - a, dom);
+    double u1 = cv / u0;
+    double v1 = jsqrt(cv * cv / (u0 * u0) - d, dom);
+    Q->D[o] = a * inusq;
+    Q->iWd[o] = sqrt(fabs(a * inusq));
+    for (int i = 1; i < dim; ++i) {
+      Q->D[o + i] = inusq;
+      Q->iWd[o + i] = jsqrt(inusq, dom);
+    }
+    Q->u[o] = inu * u0;
+    Q->v[o] = 0.0;
+    for (int i = 1; i < dim; ++i) {
+      double wbv = inu * wb[i];
+      Q->u[o + i] = u1 * wbv;
+      Q->v[o + i] = v1 * wbv;
+    }
+    double ziv = zbk[0], siv = sbk[0];
+    double tmv1 = jsqrt(jsqrt(sprod, dom) * jsqrt(zprod, dom), dom);
+    double mult = tmv1 / (ziv + siv + 2.0 * gamma);
+    for (int i = 1; i < dim; ++i) S->l[o + i] = (sbk[i] * (gamma + ziv) + zbk[i] * (gamma + siv)) * mult;
+    S->l[o] = gamma * tmv1;
+  }
+}
+
+/* dense lower Cholesky (column by column, left-looking); 0 or j+1 at a failed pivot */
+static int potrf_l(double* L, int n) {
+  for (int j = 0; j < n; ++j) {
+    double ajj = M(L, n, j, j);
+    for (int q = 0; q < j; ++q) ajj -= M(L, n, j, q) * M(L, n, j, q);
+    if (ajj <= 0.0 || isnan(ajj)) return j + 1;
+    ajj = sqrt(ajj);
+    M(L, n, j, j) = ajj;
+    for (int i = j + 1; i < n; ++i) {
+      double t = M(L, n, i, j);
+      for (int q = 0; q < j; ++q) t -= M(L, n, i, q) * M(L, n, j, q);
+      M(L, n, i, j) = t / ajj;
+    }
+    for (int i = 0; i < j; ++i) M(L, n, i, j) = 0.0;
+  }
+  return 0;
+}
+
+/* L L' +/- w w' (sig = +1 update, -1 downdate); w is overwritten; 0 or j+1 */
+static int chol_rank1(double* L, int n, double* w, double sig) {
+  for (int j = 0; j < n; ++j) {
+    double ljj = M(L, n, j, j), wj = w[j];
+    double r2 = ljj * ljj + sig * wj * wj;
+    if (r2 <= 0.0 || isnan(r2)) return j + 1;
+    double r = sqrt(r2);
+    double c = r / ljj, s = wj / ljj;
+    M(L, n, j, j) = r;
+    for (int i = j + 1; i < n; ++i) {
+      double lij = (M(L, n, i, j) + sig * s * w[i]) / c;
+      M(L, n, i, j) = lij;
+      w[i] = c * w[i] - s * lij;
+    }
+  }
+  return 0;
+}
+
+/* L y = b, then L' x = y, in place */
+static void chol_solve_l(const double* L, int n, double* b) {
+  for (int j = 0; j < n; ++j) {
+    b[j] /= M(L, n, j, j);
+    for (int i = j + 1; i < n; ++i) b[i] -= M(L, n, i, j) * b[j];
+  }
+  for (int j = n - 1; j >= 0; --j) {
+    double t = b[j];
+    for (int i = j + 1; i < n; ++i) t -= M(L, n, i, j) * b[i];
+    b[j] = t / M(L, n, j, j);
+  }
+}
+
+/* setup_iter(::SparseSolver) (spsolver.jl:60-84).  L_H in D->H, L_S in D->S,
+ * C = L^-1 A' (n x m) in D->ALi.  Returns 0 / 2 (chol of H or a downdate) / 3. */
+static int sqr_setup_iter(dense_t* D, const cones_t* C, const sqr_t* Q) {
+  int n = D->n, m = D->m, k = D->k;
+  double* L = D->H;
+  for (int b = 0; b < n; ++b)
+    for (int a = 0; a < n; ++a) {
+      double acc = 0.0;
+      if (!D->sing) /* GiW = iW G' -> factor of (iW G)'(iW G) (:62-64) */
+        for (int i = 0; i < k; ++i) acc += (Q->iWd[i] * M(D->G, k, i, a)) * (Q->iWd[i] * M(D->G, k, i, b));
+      else /* Gint = iWiW G; i1 = G' Gint + AA (:67-71) */
+        for (int i = 0; i < k; ++i) acc += M(D->G, k, i, a) * (Q->D[i] * M(D->G, k, i, b));
+      M(L, n, a, b) = acc + (D->sing ? M(D->AA, n, a, b) : 0.0);
+    }
+  if (potrf_l(L, n)) return 2;
+  /* modify_factors! (sqrscalings.jl:160-194): per SOC cone, +G'u then -G'v */
+  double* w = D->n1;
+  for (int c = 0; c < C->ncones; ++c) {
+    if (C->kind[c] != SOC) continue;
+    int o = C->offs[c], d = C->dim[c];
+    for (int pass = 0; pass < 2; ++pass) {
+      const double* uv = pass ? Q->v : Q->u;
+      for (int a = 0; a < n; ++a) {
+        double acc = 0.0;
+        for (int i = o; i < o + d; ++i) acc += M(D->G, k, i, a) * uv[i];
+        w[a] = acc;
+      }
+      if (chol_rank1(L, n, w, pass ? -1.0 : 1.0)) return 2;
+    }
+  }
+  /* C = L^-1 A' (:80-82), S = C'C, chol(S) (:83) */
+  double* Cm = D->ALi;
+  for (int r = 0; r < m; ++r) {
+    double* col = Cm + (size_t)r * n;
+    for (int a = 0; a < n; ++a) col[a] = M(D->A, m, r, a);
+    for (int j = 0; j < n; ++j) {
+      col[j] /= M(L, n, j, j);
+      for (int i = j + 1; i < n; ++i) col[i] -= M(L, n, i, j) * col[j];
+    }
+  }
+  for (int q = 0; q < m; ++q)
+    for (int r = 0; r < m; ++r) {
+      double acc = 0.0;
+      for (int a = 0; a < n; ++a) acc += Cm[(size_t)r * n + a] * Cm[(size_t)q * n + a];
+      M(D->S, m, r, q) = acc;
+    }
+  if (potrf_l(D->S, m)) return 3;
+  return 0;
+}
+
+/* solve_kkt(::SparseSolver) (spsolver.jl:86-130) */
+static void sqr_solve_kkt(dense_t* D, const cones_t* C, const scaling_t* S, const double* dx,
+                          const double* dy, const double* dz, const double* ds, double* cx, double* cy,
+                          double* cz, double* cs) {
+  int n = D->n, m = D->m, k = D->k;
+  iprod(C, D->k0, S->l, ds);
+  scale_w(C, S, D->k0, D->k1);
+  for (int i = 0; i < k; ++i) D->k2[i] = dz[i] - D->k1[i];
+  iscale_w(C, S, D->k2, D->k1);
+  iscale_w(C, S, D->k1, D->k1);
+  for (int a = 0; a < n; ++a) {
+    double acc = 0.0;
+    for (int i = 0; i < k; ++i) acc += M(D->G, k, i, a) * D->k1[i];
+    D->n0[a] = acc + dx[a];
+  }
+  if (D->sing)
+    for (int a = 0; a < n; ++a) {
+      double acc = 0.0;
+      for (int r = 0; r < m; ++r) acc += M(D->A, m, r, a) * dy[r];
+      D->n0[a] += acc;
+    }
+  for (int a = 0; a < n; ++a) D->n1[a] = D->n0[a];
+  chol_solve_l(D->H, n, D->n1);
+  for (int r = 0; r < m; ++r) {
+    double acc = 0.0;
+    for (int a = 0; a < n; ++a) acc += M(D->A, m, r, a) * D->n1[a];
+    cy[r] = acc - dy[r];
+  }
+  chol_solve_l(D->S, m, cy);
+  for (int r = 0; r < m; ++r) D->m0[r] = D->sing ? dy[r] - cy[r] : -cy[r];
+  for (int a = 0; a < n; ++a) {
+    double acc = 0.0;
+    for (int r = 0; r < m; ++r) acc += M(D->A, m, r, a) * D->m0[r];
+    D->n0[a] += acc;
+  }
+  for (int a = 0; a < n; ++a) cx[a] = D->n0[a];
+  chol_solve_l(D->H, n, cx);
+  for (int i = 0; i < k; ++i) {
+    double acc = 0.0;
+    for (int a = 0; a < n; ++a) acc += M(D->G, k, i, a) * cx[a];
+    D->k1[i] = acc - D->k2[i];
+  }
+  iscale_w(C, S, D->k1, cz);
+  iscale_w(C, S, cz, cz);
+  scale_w(C, S, cz, D->k1);
+  for (int i = 0; i < k; ++i) D->k0[i] -= D->k1[i];
+  scale_w(C, S, D->k0, cs);
+}
+
 /* ---------------- workspace ---------------- */
 
 typedef struct {
   scaling_t S;
   dense_t D;
+  sqr_t Q;
   double *rd, *rp, *rz, *rs_, *dx, *dy, *dz, *ds, *rx, *ry, *rzz, *rss, *kt1, *kt2, *kt3, *nt1,
       *nt2, *mt1, *idel;
   double *K, *rhs; /* init system (n+m+k)^2 */
@@ -555,6 +793,7 @@ static int ws_init(ws_t* w, int n, int m, int k, int ncones, int maxdim) {
   SZ(sizeof(double) * N * N);
   SZ(sizeof(double) * N);
   SZ(sizeof(int) * N);
+  SZ(sizeof(double) * 4 * k);
 #undef SZ
   need += 64 * 64; /* per-carve alignment slack */
   char* p = (char*)calloc(1, need + 64);
@@ -597,6 +836,10 @@ static int ws_init(ws_t* w, int n, int m, int k, int ncones, int maxdim) {
   w->K = carve(&p, sizeof(double) * N * N);
   w->rhs = carve(&p, sizeof(double) * N);
   w->piv = carve(&p, sizeof(int) * N);
+  w->Q.D = carve(&p, sizeof(double) * 4 * k);
+  w->Q.iWd = w->Q.D + k;
+  w->Q.u = w->Q.D + 2 * k;
+  w->Q.v = w->Q.D + 3 * k;
   return 0;
 }
 
@@ -657,6 +900,7 @@ typedef struct {
 
 #define F_WARM 2
 #define OR_F_STRUCTURED 16 /* oracle-only: the build's structured algorithm (CPU baseline) */
+#define OR_F_SQR 32        /* oracle-only: SqrScaling + SparseSolver (spsolver.jl) instead of DenseSolver */
 
 static double dot(const double* a, const double* b, int n) {
   double s = 0.0;
@@ -720,6 +964,9 @@ static void solve_one(ws_t* w, const cones_t* C, const double* c, const double* 
   D->sing = sing;
   D->C = C;
   D->structured = (P->flags & OR_F_STRUCTURED) != 0;
+  const int sqr = (P->flags & OR_F_SQR) != 0;
+#define KKT(a, b_, c_, d, e, f, g, h_) \
+  (sqr ? sqr_solve_kkt(D, C, S, a, b_, c_, d, e, f, g, h_) : solve_kkt(D, C, S, a, b_, c_, d, e, f, g, h_))
   /* DenseSolver ctor: AA = A'A (densesolver.jl:31-32) */
   for (int bq = 0; bq < n; ++bq)
     for (int a = 0; a < n; ++a) {
@@ -748,7 +995,10 @@ static void solve_one(ws_t* w, const cones_t* C, const double* c, const double* 
       memcpy(t + n + m + k, s, sizeof(double) * k);
     }
     int dom = 0;
-    compute_scaling_x(C, S, s, z, &dom, D->structured);
+    if (sqr)
+      sqr_compute_scaling(C, S, &w->Q, s, z, &dom);
+    else
+      compute_scaling_x(C, S, s, z, &dom, D->structured);
     if (dom) {
       status = 4;
       break;
@@ -779,12 +1029,12 @@ static void solve_one(ws_t* w, const cones_t* C, const double* c, const double* 
     for (int i = 0; i < m; ++i) w->dy[i] *= -1.0;
     for (int i = 0; i < k; ++i) w->dz[i] *= -1.0;
     for (int i = 0; i < k; ++i) w->ds[i] *= -1.0;
-    int st = setup_iter(D, S);
+    int st = sqr ? sqr_setup_iter(D, C, &w->Q) : setup_iter(D, S);
     if (st) {
       status = st;
       break;
     }
-    solve_kkt(D, C, S, w->dx, w->dy, w->dz, w->ds, w->rx, w->ry, w->rzz, w->rss);
+    KKT(w->dx, w->dy, w->dz, w->ds, w->rx, w->ry, w->rzz, w->rss);
     scale_w(C, S, w->rzz, w->kt3);
     iscale_w(C, S, w->rss, w->kt2);
     double t = compute_step(C, l, w->kt3, w->kt2, &dom);
@@ -803,7 +1053,7 @@ static void solve_one(ws_t* w, const cones_t* C, const double* c, const double* 
     for (int j = 0; j < n; ++j) w->dx[j] *= scfact;
     for (int i = 0; i < m; ++i) w->dy[i] *= scfact;
     for (int i = 0; i < k; ++i) w->dz[i] *= scfact;
-    solve_kkt(D, C, S, w->dx, w->dy, w->dz, w->ds, w->rx, w->ry, w->rzz, w->rss);
+    KKT(w->dx, w->dy, w->dz, w->ds, w->rx, w->ry, w->rzz, w->rss);
     scale_w(C, S, w->rzz, w->kt3);
     iscale_w(C, S, w->rss, w->kt2);
     double step = compute_step(C, l, w->kt3, w->kt2, &dom);
@@ -837,6 +1087,7 @@ done:
   }
   *iters_out = iters;
   *status_out = status;
+#undef KKT
 }
 
 static int max_dim(const cones_t* C) {
@@ -956,6 +1207,41 @@ EXPORT int or_kkt_single(int nc, const int32_t* kind, const int32_t* offs, const
       solve_kkt(&w.D, &C, &w.S, dx, dy, dz, ds, cx, cy, cz, cs);
       if (Liout) memcpy(Liout, w.D.Li, sizeof(double) * (size_t)n * n);
     }
+  }
+  ws_free(&w);
+  return st;
+}
+
+/* SqrScaling + setup_iter(::SparseSolver) + solve_kkt for one problem at (s,z)
+ * (the runtests.jl:95-128 sequence).  Optional outputs: Lout (n x n, the
+ * factor of H after modify_factors!), l/wbs (k), mu (nc).  Returns status. */
+EXPORT int or_sqr_kkt_single(int nc, const int32_t* kind, const int32_t* offs, const int32_t* dim,
+                             int n, int m, int k, const double* A, const double* G, int sing,
+                             const double* s, const double* z, const double* dx, const double* dy,
+                             const double* dz, const double* ds, double* cx, double* cy, double* cz,
+                             double* cs, double* Lout, double* lout, double* wbsout, double* muout) {
+  cones_t C = {nc, kind, offs, dim};
+  ws_t w;
+  if (ws_init(&w, n, m, k, nc, max_dim(&C))) return -1;
+  w.D.A = A;
+  w.D.G = G;
+  w.D.sing = sing;
+  w.D.C = &C;
+  for (int bq = 0; bq < n; ++bq)
+    for (int a = 0; a < n; ++a) {
+      double acc = 0.0;
+      for (int r = 0; r < m; ++r) acc += M(A, m, r, a) * M(A, m, r, bq);
+      M(w.D.AA, n, a, bq) = acc;
+    }
+  int dom = 0;
+  sqr_compute_scaling(&C, &w.S, &w.Q, s, z, &dom);
+  if (lout) memcpy(lout, w.S.l, sizeof(double) * k);
+  if (wbsout) memcpy(wbsout, w.S.wbs, sizeof(double) * k);
+  if (muout) memcpy(muout, w.S.mu, sizeof(double) * nc);
+  int st = dom ? 4 : sqr_setup_iter(&w.D, &C, &w.Q);
+  if (!st) {
+    sqr_solve_kkt(&w.D, &C, &w.S, dx, dy, dz, ds, cx, cy, cz, cs);
+    if (Lout) memcpy(Lout, w.D.H, sizeof(double) * (size_t)n * n);
   }
   ws_free(&w);
   return st;

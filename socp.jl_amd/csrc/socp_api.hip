@@ -16,6 +16,7 @@
 
 #include "../../include/socp.h"
 #include "socp_kernels.hpp"
+#include "socp_sqr.hpp"
 
 using namespace socp;
 
@@ -787,6 +788,249 @@ extern "C" int socp_dense_h2d_bytes(const socp_dense* h, int64_t* bytes) {
 
 extern "C" int64_t socp_dense_record_bytes(const socp_dense* h) {
   return h ? h->rec_stride * (int64_t)sizeof(double) : 0;
+}
+
+// ------------------------------------------------------ rank-update handles
+// SparseSolver (spsolver.jl:1-130) with SqrScaling (sqrscalings.jl): the
+// handle keeps A, G (and sing) on the device, setup_iter computes W^-2 =
+// D + uu' - vv', factors G'DG (+A'A), applies the rank-1 modifications and
+// factors S into one record per problem; solve_kkt solves against it
+// (socp_sqr.hip).
+struct socp_sqr {
+  socp_ctx* ctx = nullptr;
+  SqrArgs a;
+  SqrLayout L;
+  size_t lds = 0;
+  bool dev = false, ready = false;
+  int64_t h2d_bytes = 0;
+  enum { Q_A, Q_G, Q_SING, Q_REC, Q_S, Q_Z, Q_DX, Q_DY, Q_DZ, Q_DS, Q_CX, Q_CY, Q_CZ, Q_CS, Q_ST, Q_OUT,
+         NQB };
+  DevBuf buf[NQB];
+};
+
+static void sqr_free(socp_sqr* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->ctx->device);
+  (void)hipStreamSynchronize(h->ctx->stream);
+  for (auto& b : h->buf) b.release();
+  delete h;
+}
+
+static bool sqr_fits(const socp_dims* d, size_t* lds) {
+  if (d->n > SQR_NMAX || d->m > SQR_NMAX || d->k > SQR_KMAX) return false;
+  const size_t bytes = (size_t)sqr_layout(d->n, d->m, d->k, d->ncones).total * sizeof(double);
+  if (lds) *lds = bytes;
+  return bytes <= 160 * 1024;
+}
+
+extern "C" int socp_sqr_supported(const socp_dims* d) { return d && sqr_fits(d, nullptr) ? 1 : 0; }
+
+template <class T>
+static int sqr_in(socp_sqr* h, int slot, const T* src, size_t count, const T** out) {
+  if (!src || count == 0 || h->dev) {
+    *out = src;
+    return 0;
+  }
+  if (h->buf[slot].ensure(count * sizeof(T))) return fail(SOCP_E_NOMEM, "device allocation failed");
+  HIPCHK(hipMemcpyAsync(h->buf[slot].p, src, count * sizeof(T), hipMemcpyHostToDevice, h->ctx->stream));
+  h->h2d_bytes += (int64_t)(count * sizeof(T));
+  *out = (const T*)h->buf[slot].p;
+  return 0;
+}
+template <class T>
+static int sqr_out(socp_sqr* h, int slot, T* user, size_t count, T** out) {
+  if (!user || count == 0 || h->dev) {
+    *out = user;
+    return 0;
+  }
+  if (h->buf[slot].ensure(count * sizeof(T))) return fail(SOCP_E_NOMEM, "device allocation failed");
+  *out = (T*)h->buf[slot].p;
+  return 0;
+}
+
+extern "C" int socp_sqr_create(socp_ctx* ctx, const socp_dims* dims, const int32_t* cone_kind,
+                               const int32_t* cone_offs, const int32_t* cone_dim, const double* A,
+                               const double* G, const uint8_t* sing, int32_t flags, socp_sqr** out) {
+  if (!out) return fail(SOCP_E_INVALID, "out is NULL");
+  *out = nullptr;
+  if (!ctx) return fail(SOCP_E_INVALID, "ctx is NULL");
+  socp_sqr* h = new socp_sqr();
+  h->ctx = ctx;
+  SqrArgs& a = h->a;
+  memset(&a, 0, sizeof(a));
+  auto bail = [&](int rc) {
+    sqr_free(h);
+    return rc;
+  };
+  int degree = 0;
+  int rc = check_problem(dims, cone_kind, cone_offs, cone_dim, &a.cones, &degree);
+  if (rc) return bail(rc);
+  if (!sqr_fits(dims, &h->lds))
+    return bail(fail(SOCP_E_UNSUPPORTED, "rank-update plugin: n, m <= 64, k <= 256 (socp_sqr.hip)"));
+  const int64_t B = dims->batch;
+  const int n = dims->n, m = dims->m, k = dims->k;
+  if (B > 0 && (!G || (m > 0 && !A))) return bail(fail(SOCP_E_INVALID, "NULL data pointer"));
+  if (hipSetDevice(ctx->device) != hipSuccess) return bail(fail(SOCP_E_HIP, "hipSetDevice"));
+  h->dev = (flags & SOCP_F_DEVICE_PTRS) != 0;
+  a.B = B;
+  a.n = n;
+  a.m = m;
+  a.k = k;
+  a.nc = dims->ncones;
+  h->L = sqr_layout(n, m, k, a.nc);
+  if (B == 0) {
+    *out = h;
+    return 0;
+  }
+  typedef socp_sqr Q;
+  auto own = [&](int slot, const void* src, size_t bytes) -> int {
+    if (!src || bytes == 0) return 0;
+    if (h->buf[slot].ensure(bytes)) return fail(SOCP_E_NOMEM, "device allocation failed");
+    HIPCHK(hipMemcpyAsync(h->buf[slot].p, src, bytes, h->dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                          ctx->stream));
+    if (!h->dev) h->h2d_bytes += (int64_t)bytes;
+    return 0;
+  };
+  if ((rc = own(Q::Q_A, A, (size_t)B * m * n * sizeof(double)))) return bail(rc);
+  if ((rc = own(Q::Q_G, G, (size_t)B * k * n * sizeof(double)))) return bail(rc);
+  if ((rc = own(Q::Q_SING, sing, (size_t)B))) return bail(rc);
+  a.A = m > 0 ? (const double*)h->buf[Q::Q_A].p : nullptr;
+  a.G = (const double*)h->buf[Q::Q_G].p;
+  a.sing = sing ? (const uint8_t*)h->buf[Q::Q_SING].p : nullptr;
+  if (h->buf[Q::Q_REC].ensure((size_t)B * (size_t)h->L.rec * sizeof(double)))
+    return bail(fail(SOCP_E_NOMEM, "factor record allocation failed"));
+  a.rec = (double*)h->buf[Q::Q_REC].p;
+  const void* kerns[2] = {sqr_setup_kernel_ptr(), sqr_solve_kernel_ptr()};
+  for (const void* kern : kerns)
+    if (h->lds > 64 * 1024 &&
+        hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds) != hipSuccess)
+      return bail(fail(SOCP_E_HIP, "hipFuncSetAttribute"));
+  *out = h;
+  return 0;
+}
+
+extern "C" int socp_sqr_destroy(socp_sqr* h) {
+  sqr_free(h);
+  return 0;
+}
+
+static int sqr_launch(socp_sqr* h, const SqrArgs& a, bool setup) {
+  socp_ctx* ctx = h->ctx;
+  const void* kern = setup ? sqr_setup_kernel_ptr() : sqr_solve_kernel_ptr();
+  SqrArgs la = a;
+  void* kargs[] = {&la};
+  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(256), kargs, h->lds, ctx->stream));
+  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  ctx->last_name = setup ? "socp_sqr_setup_kernel" : "socp_sqr_solve_kernel";
+  return 0;
+}
+
+extern "C" int socp_sqr_setup_iter(socp_sqr* h, const double* s, const double* z, int32_t* status) {
+  if (!h) return fail(SOCP_E_INVALID, "handle is NULL");
+  h->h2d_bytes = 0;
+  SqrArgs a = h->a;
+  const int64_t B = a.B;
+  if (B == 0) {
+    h->ready = true;
+    return 0;
+  }
+  if (!s || !z || !status) return fail(SOCP_E_INVALID, "NULL data pointer");
+  socp_ctx* ctx = h->ctx;
+  HIPCHK(hipSetDevice(ctx->device));
+  typedef socp_sqr Q;
+  const size_t k = (size_t)a.k;
+  TRY(sqr_in(h, Q::Q_S, s, (size_t)B * k, &a.s));
+  TRY(sqr_in(h, Q::Q_Z, z, (size_t)B * k, &a.z));
+  TRY(sqr_out(h, Q::Q_ST, status, (size_t)B, &a.status));
+  TRY(sqr_launch(h, a, true));
+  if (!h->dev) {
+    HIPCHK(hipMemcpyAsync(status, a.status, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  h->ready = true;
+  return 0;
+}
+
+extern "C" int socp_sqr_solve_kkt(socp_sqr* h, const double* dx, const double* dy, const double* dz,
+                                  const double* ds, double* cx, double* cy, double* cz, double* cs,
+                                  int32_t* status) {
+  if (!h) return fail(SOCP_E_INVALID, "handle is NULL");
+  if (!h->ready) return fail(SOCP_E_INVALID, "solve_kkt before setup_iter");
+  h->h2d_bytes = 0;
+  SqrArgs a = h->a;
+  const int64_t B = a.B;
+  if (B == 0) return 0;
+  const int n = a.n, m = a.m, k = a.k;
+  if (!dx || !dz || !ds || !cx || !cz || !cs || !status || (m > 0 && (!dy || !cy)))
+    return fail(SOCP_E_INVALID, "NULL data pointer");
+  socp_ctx* ctx = h->ctx;
+  HIPCHK(hipSetDevice(ctx->device));
+  typedef socp_sqr Q;
+  TRY(sqr_in(h, Q::Q_DX, dx, (size_t)B * n, &a.dx));
+  TRY(sqr_in(h, Q::Q_DY, dy, (size_t)B * m, &a.dy));
+  TRY(sqr_in(h, Q::Q_DZ, dz, (size_t)B * k, &a.dz));
+  TRY(sqr_in(h, Q::Q_DS, ds, (size_t)B * k, &a.ds));
+  TRY(sqr_out(h, Q::Q_CX, cx, (size_t)B * n, &a.cx));
+  TRY(sqr_out(h, Q::Q_CY, cy, (size_t)B * m, &a.cy));
+  TRY(sqr_out(h, Q::Q_CZ, cz, (size_t)B * k, &a.cz));
+  TRY(sqr_out(h, Q::Q_CS, cs, (size_t)B * k, &a.cs));
+  TRY(sqr_out(h, Q::Q_ST, status, (size_t)B, &a.status));
+  TRY(sqr_launch(h, a, false));
+  TRY(copy_back(ctx, cx, a.cx, (size_t)B * n, h->dev));
+  TRY(copy_back(ctx, cy, a.cy, (size_t)B * m, h->dev));
+  TRY(copy_back(ctx, cz, a.cz, (size_t)B * k, h->dev));
+  TRY(copy_back(ctx, cs, a.cs, (size_t)B * k, h->dev));
+  TRY(copy_back(ctx, status, a.status, (size_t)B, h->dev));
+  if (!h->dev) HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+// one problem's factor of H after modify_factors! (n x n, column-major, zeros
+// above the diagonal) -- the Gfact of spsolver.jl:13 as a dense matrix
+extern "C" int socp_sqr_factor(socp_sqr* h, int64_t problem, double* L) {
+  if (!h || !L) return fail(SOCP_E_INVALID, "NULL argument");
+  if (!h->ready) return fail(SOCP_E_INVALID, "factor before setup_iter");
+  if (problem < 0 || problem >= h->a.B) return fail(SOCP_E_INVALID, "problem index out of range");
+  HIPCHK(hipSetDevice(h->ctx->device));
+  const double* src = h->a.rec + problem * h->L.rec + h->L.r_L;
+  HIPCHK(hipMemcpyAsync(L, src, (size_t)h->a.n * h->a.n * sizeof(double), hipMemcpyDefault, h->ctx->stream));
+  HIPCHK(hipStreamSynchronize(h->ctx->stream));
+  return 0;
+}
+
+// lambda (B x k), wb (B x k) and mu (B x ncones) of the last setup_iter: the
+// SqrScaling fields l, wbs, mu (sqrscalings.jl:11-16) the driver loop reads
+extern "C" int socp_sqr_scaling(socp_sqr* h, double* l, double* wbs, double* mu) {
+  if (!h) return fail(SOCP_E_INVALID, "handle is NULL");
+  if (!h->ready) return fail(SOCP_E_INVALID, "scaling before setup_iter");
+  const int64_t B = h->a.B;
+  if (B == 0) return 0;
+  HIPCHK(hipSetDevice(h->ctx->device));
+  const SqrLayout& L = h->L;
+  const int k = h->a.k, nc = h->a.nc;
+  const size_t pitch = (size_t)L.rec * sizeof(double);
+  if (l)
+    HIPCHK(hipMemcpy2DAsync(l, k * sizeof(double), h->a.rec + L.r_l, pitch, k * sizeof(double), B,
+                            hipMemcpyDefault, h->ctx->stream));
+  if (wbs)
+    HIPCHK(hipMemcpy2DAsync(wbs, k * sizeof(double), h->a.rec + L.r_wb, pitch, k * sizeof(double), B,
+                            hipMemcpyDefault, h->ctx->stream));
+  if (mu)
+    HIPCHK(hipMemcpy2DAsync(mu, nc * sizeof(double), h->a.rec + L.r_mu, pitch, nc * sizeof(double), B,
+                            hipMemcpyDefault, h->ctx->stream));
+  HIPCHK(hipStreamSynchronize(h->ctx->stream));
+  return 0;
+}
+
+extern "C" int socp_sqr_h2d_bytes(const socp_sqr* h, int64_t* bytes) {
+  if (!h || !bytes) return fail(SOCP_E_INVALID, "NULL argument");
+  *bytes = h->h2d_bytes;
+  return 0;
+}
+
+extern "C" int64_t socp_sqr_record_bytes(const socp_sqr* h) {
+  return h ? h->L.rec * (int64_t)sizeof(double) : 0;
 }
 
 // ------------------------------------------------------------- generator

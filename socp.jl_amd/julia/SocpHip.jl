@@ -190,6 +190,57 @@ function solve_kkt(ss::HipDenseSolver, pr::Problem{C,n,m,k,sing}, s::State, scal
     return nothing
 end
 
+# ---------------------------------------------------- rank-update plugin
+# HipSqrSolver replaces SparseSolver (spsolver.jl:1-130) -- the solver the
+# reference's own tests and MOI wrapper run -- on the device (include/socp.h,
+# socp_sqr_*): SqrScaling's W^-2 = D + uu' - vv' (sqrscalings.jl:66-139), the
+# factor of G'DG (+A'A), one rank-1 update and one downdate per SOC cone
+# (modify_factors!, sqrscalings.jl:160-194) and the factor of S, all inside
+# setup_iter; solve_kkt by triangular solves.  Its scaling type is the same
+# HipScaling: SqrScaling's l, wbs, mu equal Scaling's (runtests.jl:58-60,71-73),
+# and the driver loop reads nothing else.  Usage:
+#     ss = SolverState(prob, HipSqrSolver(prob)); solve_socp(prob, ss)
+mutable struct HipSqrSolver <: KKTSolver{HipScaling}
+    handle::Ptr{Cvoid}
+    status::Vector{Int32}
+    function HipSqrSolver(pr::Problem{C,n,m,k,sing}) where {C,n,m,k,sing}
+        kind, offs, dim = cone_arrays(pr.cones)
+        dims = Ref(SocpDims(1, n, m, k, length(pr.cones)))
+        A = Matrix{Float64}(pr.A)
+        G = Matrix{Float64}(pr.G)
+        singv = UInt8[sing ? 1 : 0]
+        h = Ref{Ptr{Cvoid}}(C_NULL)
+        socp_check(ccall((:socp_sqr_create, libsocp), Cint,
+                         (Ptr{Cvoid}, Ref{SocpDims}, Ptr{Int32}, Ptr{Int32}, Ptr{Int32},
+                          Ptr{Float64}, Ptr{Float64}, Ptr{UInt8}, Int32, Ptr{Ptr{Cvoid}}),
+                         socp_ctx(), dims, kind, offs, dim, A, G, singv, Int32(0), h))
+        ss = new(h[], Int32[0])
+        finalizer(ss) do x
+            x.handle == C_NULL || ccall((:socp_sqr_destroy, libsocp), Cint, (Ptr{Cvoid},), x.handle)
+            x.handle = C_NULL
+        end
+        return ss
+    end
+end
+
+function setup_iter(ss::HipSqrSolver, pr::Problem{C,n,m,k,sing}, s::State, scaling::HipScaling) where {C,n,m,k,sing}
+    socp_check(ccall((:socp_sqr_setup_iter, libsocp), Cint,
+                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}), ss.handle, s.s, s.z, ss.status))
+    socp_throw(ss.status[1])
+    return nothing
+end
+
+function solve_kkt(ss::HipSqrSolver, pr::Problem{C,n,m,k,sing}, s::State, scaling::HipScaling,
+                   dx::Vector{Float64}, dy::Vector{Float64}, dz::Vector{Float64}, ds::Vector{Float64},
+                   cx::Vector{Float64}, cy::Vector{Float64}, cz::Vector{Float64}, cs::Vector{Float64}) where {C,n,m,k,sing}
+    socp_check(ccall((:socp_sqr_solve_kkt, libsocp), Cint,
+                     (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                      Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                     ss.handle, dx, dy, dz, ds, cx, cy, cz, cs, ss.status))
+    socp_throw(ss.status[1])
+    return nothing
+end
+
 # ------------------------------------------------------------ batched solve
 """
     solve_socp_batched(problems; maxit=40, tol=1e-5) -> (states, iters, status)

@@ -228,8 +228,12 @@ class DenseHandle:
     argument must be a device tensor too; calls are stream-ordered on torch's
     current stream.  Results are bitwise those of ``batch_kkt_solve``."""
 
+    _pfx = "socp_dense"
+
+    def _fn(self, name):
+        return getattr(_lib.load(), f"{self._pfx}_{name}")
+
     def __init__(self, cones, n, m, k, A, G, sing=None, *, ctx=None, force_large=False):
-        L = _lib.load()
         self.cones, self.n, self.m, self.k = cones, n, m, k
         self.kind, self.offs, self.dim = cone_arrays(cones)
         B = _size(G) // (k * n)
@@ -248,13 +252,13 @@ class DenseHandle:
         h = C.c_void_p()
         dims = _lib.Dims(B, n, m, k, len(self.kind))
         p = _lib.ptr
-        _lib.check(L.socp_dense_create(self.ctx.handle, dims, p(self.kind), p(self.offs), p(self.dim),
+        _lib.check(self._fn("create")(self.ctx.handle, dims, p(self.kind), p(self.offs), p(self.dim),
                                        p(arrs[0]), p(arrs[1]), p(arrs[2]), flags, C.byref(h)))
         self.handle = h
 
     def close(self):
         if getattr(self, "handle", None):
-            _lib.load().socp_dense_destroy(self.handle)
+            self._fn("destroy")(self.handle)
             self.handle = None
 
     def __del__(self):
@@ -284,7 +288,7 @@ class DenseHandle:
         if self.dev:
             self.ctx.bind_torch_stream()
         p = _lib.ptr
-        _lib.check(_lib.load().socp_dense_setup_iter(self.handle, p(self._arg(s)), p(self._arg(z)), p(status)))
+        _lib.check(self._fn("setup_iter")(self.handle, p(self._arg(s)), p(self._arg(z)), p(status)))
         return status
 
     def solve_kkt(self, dx, dy, dz, ds, out=None):
@@ -305,7 +309,7 @@ class DenseHandle:
         if self.dev:
             self.ctx.bind_torch_stream()
         p = _lib.ptr
-        _lib.check(_lib.load().socp_dense_solve_kkt(
+        _lib.check(self._fn("solve_kkt")(
             self.handle, p(self._arg(dx)), p(self._arg(dy) if m else None), p(self._arg(dz)),
             p(self._arg(ds)), p(out["cx"]), p(out["cy"] if m else None), p(out["cz"]), p(out["cs"]),
             p(out["status"])))
@@ -317,13 +321,47 @@ class DenseHandle:
     def h2d_bytes(self) -> int:
         """Host-to-device bytes moved by the last call (socp_dense_h2d_bytes)."""
         v = C.c_int64()
-        _lib.check(_lib.load().socp_dense_h2d_bytes(self.handle, C.byref(v)))
+        _lib.check(self._fn("h2d_bytes")(self.handle, C.byref(v)))
         return int(v.value)
 
     @property
     def record_bytes(self) -> int:
         """Device bytes of one problem's factor record."""
-        return int(_lib.load().socp_dense_record_bytes(self.handle))
+        return int(self._fn("record_bytes")(self.handle))
+
+
+class SqrHandle(DenseHandle):
+    """A batch of SparseSolver objects with SqrScaling on the device
+    (socp_sqr_*, the reference's rank-update path: spsolver.jl,
+    sqrscalings.jl).  ``setup_iter(s, z)`` computes W^-2 = D + uu' - vv',
+    factors G'DG (+A'A), applies one rank-1 update (G'u) and one downdate (G'v)
+    per SOC cone and factors S; ``solve_kkt`` solves by triangular solves.
+    Same call conventions as DenseHandle; n, m <= 64, k <= 256."""
+
+    _pfx = "socp_sqr"
+
+    def __init__(self, cones, n, m, k, A, G, sing=None, *, ctx=None):
+        super().__init__(cones, n, m, k, A, G, sing, ctx=ctx)
+
+    def factor(self, problem: int):
+        """The factor L of H after modify_factors! for one problem (n x n lower
+        triangular numpy array; L L' = G'W^-2 G (+A'A)) -- the Gfact of spsolver.jl:13."""
+        out = np.zeros(self.n * self.n)
+        _lib.check(self._fn("factor")(self.handle, int(problem), _lib.ptr(out)))
+        return out.reshape(self.n, self.n, order="F")
+
+    def scaling(self):
+        """dict(l, wbs, mu) of the last setup_iter for every problem (host arrays
+        B x k, B x k, B x ncones): the SqrScaling fields the driver loop reads."""
+        B, k, nc = self.B, self.k, len(self.kind)
+        l, wbs, mu = np.zeros(B * k), np.zeros(B * k), np.zeros(B * nc)
+        _lib.check(self._fn("scaling")(self.handle, _lib.ptr(l), _lib.ptr(wbs), _lib.ptr(mu)))
+        return dict(l=l.reshape(B, k), wbs=wbs.reshape(B, k), mu=mu.reshape(B, nc))
+
+
+def sqr_supported(n, m, k, ncones) -> bool:
+    """Whether the rank-update plugin takes these dims (socp_sqr_supported)."""
+    return bool(_lib.load().socp_sqr_supported(_lib.Dims(1, n, m, k, ncones)))
 
 
 def _csc_arrays(mats, rows, cols, index_base):
@@ -590,6 +628,40 @@ class DenseSolver:
 HipDenseSolver = DenseSolver
 
 
+class SqrScaling(Scaling):
+    """SqrScaling (sqrscalings.jl:8-48), the scaling type of SparseSolver: the
+    factored W^-2 = D + uu' - vv' is computed on the device by setup_iter; this
+    object records (s, z) and, after setup_iter, holds the fields the driver
+    loop reads (l, wbs, mu), read back from the device."""
+
+    def __init__(self, prob: Problem):
+        super().__init__(prob)
+        self.l = np.zeros(prob.k)
+        self.wbs = np.zeros(prob.k)
+        self.mu = np.zeros(len(prob.cones))
+
+
+class SparseSolver(DenseSolver):
+    """KKTSolver{SqrScaling} plugin (spsolver.jl:1-130) on MI355X: the
+    rank-update path -- G'DG factored, one rank-1 update and one downdate per
+    SOC cone, triangular solves (a one-problem SqrHandle).  The reference runs
+    it through CHOLMOD; here the factor is dense and LDS-resident.  The plugin
+    methods are setup_iter / solve_kkt; the whole-batch device solver
+    (solve_socp) runs the dense elimination, which computes the same KKT
+    solutions to rounding."""
+
+    scaling_type = SqrScaling
+
+    def __init__(self, prob: Problem, ctx: Context | None = None):
+        self.prob = prob
+        self.ctx = ctx
+        self.handle = SqrHandle(prob.cones, prob.n, prob.m, prob.k, _colmajor(prob.A, prob.m, prob.n),
+                                _colmajor(prob.G, prob.k, prob.n), np.array([prob.sing], np.uint8), ctx=ctx)
+
+
+HipSqrSolver = SparseSolver
+
+
 def setup_iter(solver: DenseSolver, prob: Problem, state: State, scaling: Scaling):
     """setup_iter(::DenseSolver, ...) (densesolver.jl:41-52): scaling, H, H^-1,
     A H^-1 A' and its factorisation, kept on the device.  Raises
@@ -597,6 +669,9 @@ def setup_iter(solver: DenseSolver, prob: Problem, state: State, scaling: Scalin
     sqrt does."""
     st = solver.handle.setup_iter(scaling.s, scaling.z)
     _raise_status(int(st[0]))
+    if isinstance(scaling, SqrScaling) and isinstance(solver.handle, SqrHandle):
+        sc = solver.handle.scaling()
+        scaling.l, scaling.wbs, scaling.mu = sc["l"][0], sc["wbs"][0], sc["mu"][0]
 
 
 def _raise_status(st):

@@ -31,6 +31,8 @@ EXPORTED = [
     "socp_dense_record_bytes", "socp_dense_destroy",
     "socp_ingest_create", "socp_ingest_next_inputs", "socp_ingest_submit", "socp_ingest_submit_csc",
     "socp_ingest_wait", "socp_ingest_destroy",
+    "socp_sqr_supported", "socp_sqr_create", "socp_sqr_setup_iter", "socp_sqr_solve_kkt", "socp_sqr_factor",
+    "socp_sqr_scaling", "socp_sqr_h2d_bytes", "socp_sqr_record_bytes", "socp_sqr_destroy",
 ]
 
 OUTCOME_BYTES = 32  # sizeof(socp_outcome): int32 status, int32 iters, double rd, rp, gap
@@ -112,6 +114,17 @@ def load():
         L.socp_dense_record_bytes.argtypes = [vp]
         L.socp_dense_record_bytes.restype = C.c_int64
         L.socp_dense_destroy.argtypes = [vp]
+    if hasattr(L, "socp_sqr_create"):  # rank-update plugin (absent from older A/B builds)
+        L.socp_sqr_supported.argtypes = [C.POINTER(Dims)]
+        L.socp_sqr_create.argtypes = common + [dp, dp, u8p, C.c_int32, C.POINTER(C.c_void_p)]
+        L.socp_sqr_setup_iter.argtypes = [vp, dp, dp, i32p]
+        L.socp_sqr_solve_kkt.argtypes = [vp] + [dp] * 8 + [i32p]
+        L.socp_sqr_factor.argtypes = [vp, C.c_int64, dp]
+        L.socp_sqr_scaling.argtypes = [vp, dp, dp, dp]
+        L.socp_sqr_h2d_bytes.argtypes = [vp, C.POINTER(C.c_int64)]
+        L.socp_sqr_record_bytes.argtypes = [vp]
+        L.socp_sqr_record_bytes.restype = C.c_int64
+        L.socp_sqr_destroy.argtypes = [vp]
     if hasattr(L, "socp_ingest_create"):  # pipelined ingest (absent from older A/B builds)
         L.socp_ingest_create.argtypes = common + [C.c_int32, C.POINTER(C.c_void_p)]
         L.socp_ingest_next_inputs.argtypes = [vp] + [C.POINTER(C.c_void_p)] * 6

@@ -112,3 +112,14 @@ def test_host_arrays_are_size_checked():
     with pytest.raises(ValueError, match="dz"):
         S.batch_kkt_solve(cfg.cones, n, m, k, good["A"], good["G"], None, np.zeros(B * k), np.zeros(B * k),
                           np.zeros(B * n), np.zeros(B * m), np.zeros(B * k + 3), np.zeros(B * k))
+
+
+def test_sqr_supported_dims():
+    # the rank-update plugin: n, m <= 64, k <= 256 (socp_sqr.hpp)
+    L = _lib.load()
+    for name, ok in (("C0b", True), ("C1", True), ("C2", True), ("C4", False)):
+        cfg = CONFIGS[name]
+        d = _lib.Dims(cfg.batch, cfg.n, cfg.m, cfg.k, len(cfg.cones))
+        assert bool(L.socp_sqr_supported(C.byref(d))) == ok, name
+    assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, 65, 0, 10, 1)))
+    assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, 64, 0, 257, 1)))

@@ -1,0 +1,222 @@
+"""The rank-update plugin (socp_sqr_*): SqrScaling + SparseSolver
+(sqrscalings.jl:8-214, spsolver.jl:1-130) on the GPU.
+
+Gates (fp64; CHOLMOD's permutation and supernodal order are replaced by a
+dense factor, so agreement is to rounding, never bitwise):
+  * the reference's KKT golden (runtests.jl:95-128 -- produced on exactly this
+    path) through the HIP plugin <= 1e-10;
+  * the factor after modify_factors! inverts to the dense H^-1
+    (runtests.jl:62-77) <= 1e-10, and l, wbs, mu equal the dense scaling's
+    (runtests.jl:58-60, 71-73);
+  * batches at the C1/C2 shapes at interior iterates: HIP vs the oracle's
+    rank-update restatement, rel <= 1e-9 where kappa(H) <= 1e5; HIP sqr vs the
+    HIP dense plugin at the same tolerance; m = 0 and sing problems;
+  * failures (domain error, lost definiteness in a downdate) stay in their
+    problem; solve_kkt before setup_iter is refused; per-call H2D bytes.
+"""
+import numpy as np
+import pytest
+
+import socp_amd as S
+from socp_amd.configs import C1, C2
+
+pytestmark = pytest.mark.gpu
+
+
+def iterates(oracle, cfg, B, K):
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                           sing=np.zeros(B, np.uint8), params=oracle.Params(maxit=K, tol=0.0))
+    return dict(A=d["A"], G=d["G"], s=r["s"], z=r["z"])
+
+
+def rhs(cfg, B, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.standard_normal(B * q) for q in (cfg.n, cfg.m, cfg.k, cfg.k)]
+
+
+def per_problem(v, B):
+    return v.reshape(B, -1)
+
+
+def test_sqr_kkt_golden_through_hip(kats):
+    g = kats["kkt_golden"]
+    cones = [tuple(c) for c in g["cones"]]
+    G = np.array(g["G"], dtype=np.float64)
+    k, n = G.shape
+    h = S.SqrHandle(cones, n, 0, k, None, G.ravel(order="F"))
+    st = h.setup_iter(np.array(g["s"]), np.array(g["z"]))
+    assert st[0] == 0
+    out = h.solve_kkt(np.array(g["dx"]), None, np.array(g["dz"]), np.array(g["ds"]))
+    assert out["status"][0] == 0
+    for key in ("cx", "cz", "cs"):
+        assert np.abs(out[key] - np.array(g[key])).max() < 1e-10, key
+
+
+def test_sqr_kkt_golden_through_mirror(kats):
+    # the reference's own call sequence: SparseSolver(prob), setup_iter, solve_kkt
+    g = kats["kkt_golden"]
+    cones = [S.POC(0, 1), S.SOC(1, 3)]
+    prob = S.Problem([-1.0, -1.0, 1.0], np.zeros((0, 3)), np.zeros(0), np.array(g["G"]), [5.0, 0, 0, 0], cones)
+    solver = S.SparseSolver(prob)
+    state = S.State(prob, np.zeros(3), np.zeros(0), g["z"], g["s"])
+    sc = S.compute_scaling(prob.cones, S.SqrScaling(prob), state.s, state.z)
+    S.setup_iter(solver, prob, state, sc)
+    cx, cy, cz, cs = np.zeros(3), np.zeros(0), np.zeros(4), np.zeros(4)
+    S.solve_kkt(solver, prob, state, sc, np.array(g["dx"]), np.zeros(0), np.array(g["dz"]), np.array(g["ds"]),
+                cx, cy, cz, cs)
+    for key, v in (("cx", cx), ("cz", cz), ("cs", cs)):
+        assert np.abs(v - np.array(g[key])).max() < 1e-10, key
+    assert np.all(sc.l > 0) and sc.mu[1] > 0
+
+
+def test_sqr_factor_and_scaling_match_dense(kats, oracle):
+    q = kats["sqr_scaling"]
+    cones = [tuple(c) for c in q["cones"]]
+    G = np.array(q["G"], dtype=np.float64)
+    k, n = G.shape
+    pairs = q["pairs"]
+    B = len(pairs)
+    s = np.concatenate([p["s"] for p in pairs])
+    z = np.concatenate([p["z"] for p in pairs])
+    h = S.SqrHandle(cones, n, 0, k, None, np.tile(G.ravel(order="F"), B))
+    assert (h.setup_iter(s, z) == 0).all()
+    sc_dev = h.scaling()
+    for p, pair in enumerate(pairs):
+        sc = oracle.compute_scaling(cones, np.array(pair["s"]), np.array(pair["z"]))
+        L = h.factor(p)
+        assert np.abs(np.triu(L, 1)).max() == 0.0
+        Hd = G.T @ sc["iWiW"] @ G
+        assert np.abs(np.linalg.inv(L @ L.T) - np.linalg.inv(Hd)).max() < 1e-10
+        assert np.abs(sc_dev["l"][p] - sc["l"]).max() < 1e-12
+        assert np.abs(sc_dev["wbs"][p] - sc["wbs"]).max() < 1e-12
+        assert abs(sc_dev["mu"][p][1] - sc["mu"][1]) < 1e-12
+
+
+@pytest.mark.parametrize("cfg,K", [(C1, 2), (C2, 3), (C2, 6)])
+def test_sqr_batch_matches_oracle(oracle, cfg, K):
+    B = 64
+    it = iterates(oracle, cfg, B, K)
+    h = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, it["A"], it["G"], np.zeros(B, np.uint8))
+    st = h.setup_iter(it["s"], it["z"])
+    r = rhs(cfg, B, 7)
+    got = h.solve_kkt(*r)
+    dense = S.DenseHandle(cfg.cones, cfg.n, cfg.m, cfg.k, it["A"], it["G"], np.zeros(B, np.uint8))
+    dst = dense.setup_iter(it["s"], it["z"])
+    dref = dense.solve_kkt(*r)
+    n, m, k = cfg.n, cfg.m, cfg.k
+    checked = 0
+    for p in range(B):
+        A = it["A"][p * m * n:(p + 1) * m * n].reshape(n, m).T
+        G = it["G"][p * k * n:(p + 1) * k * n].reshape(n, k).T
+        sl = lambda v, q: v[p * q:(p + 1) * q]  # noqa: E731
+        o = oracle.sqr_kkt_single(cfg.cones, A, G, False, sl(it["s"], k), sl(it["z"], k), sl(r[0], n), sl(r[1], m),
+                                  sl(r[2], k), sl(r[3], k))
+        assert st[p] == o["status"] == dst[p], p
+        if o["status"]:
+            continue
+        L = o["L"]
+        kappa = np.linalg.cond(L @ L.T)
+        if kappa > 1e5:
+            continue
+        checked += 1
+        for key, q in (("cx", n), ("cy", m), ("cz", k), ("cs", k)):
+            ref = o[key]
+            scale = max(np.abs(ref).max(), 1e-300)
+            assert np.abs(sl(got[key], q) - ref).max() <= 1e-9 * scale, (p, key)
+            assert np.abs(sl(got[key], q) - sl(dref[key], q)).max() <= 1e-9 * scale, (p, key, "vs dense")
+    assert checked >= B // 2
+
+
+def test_sqr_m0_and_sing(oracle):
+    """m = 0 (no equality rows) and a sing problem (G'G singular: the A'A term
+    enters H, spsolver.jl:66-71; the sing branch m0 = dy - cy, :115-118)."""
+    rng = np.random.default_rng(3)
+    cones = [(0, 0, 4), (1, 4, 6)]
+    n, k = 6, 10
+    for m, sing in ((0, False), (3, True)):
+        B = 8
+        G = rng.standard_normal((B, k, n))
+        if sing:
+            G[:, :, -1] = 0.0  # last column unused by the cones: G'G singular
+        A = rng.standard_normal((B, m, n))
+        s = np.zeros((B, k))
+        z = np.zeros((B, k))
+        for arr in (s, z):
+            arr[:, :4] = rng.uniform(0.5, 2.0, (B, 4))
+            arr[:, 5:] = rng.uniform(-0.3, 0.3, (B, 5))
+            arr[:, 4] = np.linalg.norm(arr[:, 5:], axis=1) + rng.uniform(0.2, 1.0, B)
+        Gf = np.concatenate([G[p].ravel(order="F") for p in range(B)])
+        Af = np.concatenate([A[p].ravel(order="F") for p in range(B)]) if m else None
+        singv = np.full(B, 1 if sing else 0, np.uint8)
+        h = S.SqrHandle(cones, n, m, k, Af, Gf, singv)
+        assert (h.setup_iter(s.ravel(), z.ravel()) == 0).all()
+        r = [rng.standard_normal(B * q) for q in (n, m, k, k)]
+        got = h.solve_kkt(r[0], r[1] if m else None, r[2], r[3])
+        for p in range(B):
+            sl = lambda v, q: v[p * q:(p + 1) * q]  # noqa: E731
+            o = oracle.sqr_kkt_single(cones, A[p], G[p], sing, s[p], z[p], sl(r[0], n), sl(r[1], m), sl(r[2], k),
+                                      sl(r[3], k))
+            assert o["status"] == 0
+            for key, q in (("cx", n), ("cy", m), ("cz", k), ("cs", k)):
+                if q == 0:
+                    continue
+                assert np.abs(sl(got[key], q) - o[key]).max() <= 1e-9 * max(1.0, np.abs(o[key]).max()), (m, p, key)
+
+
+def test_sqr_failures_are_isolated(oracle):
+    cfg, B = C2, 16
+    it = iterates(oracle, cfg, B, 2)
+    s, z = it["s"].copy(), it["z"].copy()
+    k = cfg.k
+    s[3 * k + 40] = -50.0                 # problem 3: s outside its SOC -> sqrt of a negative (DomainError)
+    z[5 * k + 2] = -1.0                   # problem 5: POC z < 0 -> z/s < 0 -> DomainError
+    h = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, it["A"], it["G"], np.zeros(B, np.uint8))
+    st = h.setup_iter(s, z)
+    assert st[3] == S.DOMAIN_ERROR and st[5] == S.DOMAIN_ERROR
+    good = [p for p in range(B) if p not in (3, 5)]
+    assert (st[good] == 0).all()
+    r = rhs(cfg, B, 1)
+    out = h.solve_kkt(*r)
+    assert out["status"][3] == S.DOMAIN_ERROR
+    assert np.isnan(out["cx"][3 * cfg.n:4 * cfg.n]).all()
+    clean = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, it["A"], it["G"], np.zeros(B, np.uint8))
+    clean.setup_iter(it["s"], it["z"])
+    ref = clean.solve_kkt(*r)
+    for p in good:  # neighbours are untouched, bit for bit
+        assert np.array_equal(out["cx"][p * cfg.n:(p + 1) * cfg.n], ref["cx"][p * cfg.n:(p + 1) * cfg.n])
+
+
+def test_sqr_refuses_solve_before_setup_and_counts_bytes(oracle):
+    cfg, B = C1, 8
+    it = iterates(oracle, cfg, B, 1)
+    h = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, it["A"], it["G"], np.zeros(B, np.uint8))
+    with pytest.raises(S.SocpError):
+        h.solve_kkt(*rhs(cfg, B, 0))
+    h.setup_iter(it["s"], it["z"])
+    assert h.h2d_bytes == B * 2 * cfg.k * 8
+    h.solve_kkt(*rhs(cfg, B, 0))
+    assert h.h2d_bytes == B * (cfg.n + cfg.m + 2 * cfg.k) * 8
+    assert h.record_bytes >= (cfg.n * cfg.n + cfg.m * cfg.m + 2 * cfg.k) * 8
+
+
+def test_sqr_device_tensors_equal_host():
+    import torch
+    cfg, B = C2, 32
+    d = S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    c, A, b, G, hh = d
+    out = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, c, A, b, G, hh, torch.zeros(B, dtype=torch.uint8,
+                        device=G.device), maxit=3, tol=0.0)
+    S.default_context().sync()
+    s, z = out["s"], out["z"]
+    hd = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, A, G, torch.zeros(B, dtype=torch.uint8, device=G.device))
+    hh_ = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, A.cpu().numpy(), G.cpu().numpy(), np.zeros(B, np.uint8))
+    std = hd.setup_iter(s, z)
+    sth = hh_.setup_iter(s.cpu().numpy(), z.cpu().numpy())
+    r = rhs(cfg, B, 4)
+    od = hd.solve_kkt(*[torch.from_numpy(v).to(G.device) for v in r])
+    torch.cuda.synchronize()
+    oh = hh_.solve_kkt(*r)
+    assert np.array_equal(std.cpu().numpy(), sth)
+    for key in ("cx", "cy", "cz", "cs"):
+        assert np.array_equal(od[key].cpu().numpy(), oh[key]), key

@@ -180,3 +180,64 @@ def test_structured_mode_matches_reference_order(oracle):
         assert (r["status"] == s["status"]).all()
         for key in ("x", "z", "s"):
             assert np.linalg.norm(r[key] - s[key]) <= 1e-9 * np.linalg.norm(r[key]), (cfg.name, key)
+
+
+# ---------------------------------------------------------------- rank-update path
+def test_sqr_oracle_kkt_golden(kats, oracle):
+    # runtests.jl:95-128 runs exactly this: SqrScaling + SparseSolver setup_iter/solve_kkt
+    g = kats["kkt_golden"]
+    cones = [tuple(c) for c in g["cones"]]
+    r = oracle.sqr_kkt_single(cones, np.zeros((0, 3)), np.array(g["G"]), False, np.array(g["s"]), np.array(g["z"]),
+                              np.array(g["dx"]), np.zeros(0), np.array(g["dz"]), np.array(g["ds"]))
+    assert r["status"] == 0
+    for key in ("cx", "cz", "cs"):
+        assert np.abs(r[key] - np.array(g[key])).max() < 1e-10, key
+
+
+def test_sqr_oracle_factor_matches_dense_inverse(kats, oracle):
+    # runtests.jl:62-77: after modify_factors!, f2 \ I == (G' iWiW G) \ I (reference: 1e-2)
+    q = kats["sqr_scaling"]
+    cones = [tuple(c) for c in q["cones"]]
+    G = np.array(q["G"], dtype=np.float64)
+    n, k = G.shape[1], G.shape[0]
+    for pair in q["pairs"]:
+        s, z = np.array(pair["s"]), np.array(pair["z"])
+        r = oracle.sqr_kkt_single(cones, np.zeros((0, n)), G, False, s, z, np.zeros(n), np.zeros(0),
+                                  np.zeros(k), np.zeros(k))
+        assert r["status"] == 0
+        sc = oracle.compute_scaling(cones, s, z)
+        Hd = G.T @ sc["iWiW"] @ G
+        L = r["L"]
+        assert np.abs(np.triu(L, 1)).max() == 0.0
+        assert np.abs(np.linalg.inv(L @ L.T) - np.linalg.inv(Hd)).max() < 1e-10
+        # runtests.jl:58-60, 71-73: SqrScaling's l, wbs, mu equal Scaling's
+        for key in ("l", "wbs"):
+            assert np.abs(r[key] - sc[key]).max() < 1e-12, key
+        soc = [i for i, c in enumerate(cones) if c[0] == 1]
+        assert np.abs(r["mu"][soc] - sc["mu"][soc]).max() < 1e-12
+
+
+@pytest.mark.parametrize("name", ["soc1", "soc2", "soc3"])
+def test_sqr_oracle_end_to_end_kats(kats, oracle, name):
+    # runtests.jl:130-191 solve these with the sparse state (SparseSolver + SqrScaling)
+    q = kats[name]
+    cones, c, A, b, G, h = kat_problem(q)
+    r = oracle.solve_trace(cones, c, A, b, G, h, params=oracle.Params(flags=oracle.F_SQR))
+    assert r["status"] == 0
+    assert np.linalg.norm(r["x"] - np.array(q["x_expect"])) < q["tol"]
+
+
+def test_sqr_oracle_matches_dense_oracle_trajectories(oracle):
+    """Both plugins solve the same KKT system: the rank-update restatement's
+    trajectory equals the dense one's inside the healthy window."""
+    from socp_amd.configs import C1, C2
+    for cfg, K in ((C1, 3), (C2, 5)):
+        B = 8
+        d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+        args = (cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"])
+        r = oracle.batch_solve(*args, sing=np.zeros(B, np.uint8), params=oracle.Params(maxit=K, tol=0.0))
+        s = oracle.batch_solve(*args, sing=np.zeros(B, np.uint8),
+                               params=oracle.Params(maxit=K, tol=0.0, flags=oracle.F_SQR))
+        assert (r["status"] == s["status"]).all()
+        for key in ("x", "z", "s"):
+            assert np.linalg.norm(r[key] - s[key]) <= 1e-8 * np.linalg.norm(r[key]), (cfg.name, key)
