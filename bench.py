@@ -270,6 +270,11 @@ def sqr_bench(args):
     ms_solve = sum(t_solve) / len(t_solve)
     st = torch.bincount(out["status"].long(), minlength=5).tolist()
     fs, fv, bs, bv = sqr_model(n, m, k, cfg.cones)
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        tj = json.load(open(args.traffic_json))
+        if tj.get("batch") == B and "socp_sqr_setup_kernel" in tj.get("kernels", []):
+            traffic = tj["hbm_bytes_per_launch"]
     setup_gbs = bs * B / (ms_setup * 1e-3) / 1e9
     solve_gbs = bv * B / (ms_solve * 1e-3) / 1e9
     dominant = "setup" if ms_setup >= 2 * ms_solve else "solve"
@@ -288,7 +293,9 @@ def sqr_bench(args):
         "kernels": {"socp_sqr_setup_kernel_ms": ms_setup, "socp_sqr_solve_kernel_ms": ms_solve},
         "status_counts": st,
         "roofline": {"bound": "hbm", "kernel": f"socp_sqr_{dominant}_kernel", "achieved": ach,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                     "traffic": traffic if dominant == "setup" else None,
+                     "hbm_gbs": traffic / (ms_setup * 1e-3) / 1e9 if traffic and dominant == "setup" else None,
                      "setup_GBps": setup_gbs, "solve_GBps": solve_gbs,
                      "setup_TFLOPs": fs * B / (ms_setup * 1e-3) / 1e12,
                      "solve_TFLOPs": fv * B / (ms_solve * 1e-3) / 1e12,

@@ -900,7 +900,7 @@ extern "C" int socp_sqr_create(socp_ctx* ctx, const socp_dims* dims, const int32
   if (h->buf[Q::Q_REC].ensure((size_t)B * (size_t)h->L.rec * sizeof(double)))
     return bail(fail(SOCP_E_NOMEM, "factor record allocation failed"));
   a.rec = (double*)h->buf[Q::Q_REC].p;
-  const void* kerns[2] = {sqr_setup_kernel_ptr(), sqr_solve_kernel_ptr()};
+  const void* kerns[2] = {sqr_setup_kernel_ptr(n), sqr_solve_kernel_ptr(n)};
   for (const void* kern : kerns)
     if (h->lds > 64 * 1024 &&
         hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds) != hipSuccess)
@@ -916,11 +916,12 @@ extern "C" int socp_sqr_destroy(socp_sqr* h) {
 
 static int sqr_launch(socp_sqr* h, const SqrArgs& a, bool setup) {
   socp_ctx* ctx = h->ctx;
-  const void* kern = setup ? sqr_setup_kernel_ptr() : sqr_solve_kernel_ptr();
+  const void* kern = setup ? sqr_setup_kernel_ptr(a.n) : sqr_solve_kernel_ptr(a.n);
   SqrArgs la = a;
+  la.stamps = setup ? g_stamps : nullptr;
   void* kargs[] = {&la};
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
-  HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(256), kargs, h->lds, ctx->stream));
+  HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(64), kargs, h->lds, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
   ctx->last_name = setup ? "socp_sqr_setup_kernel" : "socp_sqr_solve_kernel";
   return 0;

@@ -6,15 +6,20 @@
 // triangular solves.  CHOLMOD (the reference's factoriser) is replaced by a
 // dense LDS-resident factor: the batch's problems are small and dense.
 //
-// One 256-thread workgroup (4 wavefronts) per problem, n, m <= 64, k <= 256.
-//   setup kernel: s, z -> scaling (one wavefront per cone), H in 4x4
-//     register blocks from G row chunks staged through LDS, right-looking
-//     Cholesky in LDS, the rank-1 modifications and the triangular solves on
-//     wavefront 0 with one row per lane (pivot values by readlane), the
-//     factor record (L_H, L_S, lambda, wb, mu, status) to HBM.
-//   solve kernel: the record back into LDS, cone ops per wavefront, G'v / Gv
-//     mat-vecs over all four wavefronts, the four H and two S triangular
-//     solves on wavefront 0.
+// One wavefront per problem, n, m <= 64, k <= 256, register-resident: lane i
+// holds row i of H and then of its factor L in NC (= n rounded up to 16)
+// VGPR pairs; nothing in the factorisation waits on a barrier or an LDS round
+// trip -- pivots and pivot-column entries come from readlane.
+//   setup kernel: s, z -> scaling (per cone, wave reductions); H rows
+//     accumulated from G row chunks staged through LDS (broadcast reads);
+//     right-looking Cholesky in registers; per SOC cone the update (G'u) and
+//     the downdate (G'v) as two chains skewed by one column; L^-1 A' by
+//     forward substitution, S = C'C and chol(S) in LDS; the factor record
+//     (L_H, L_S, lambda, wb, mu, status) to HBM.
+//   solve kernel: L rows back into registers; forward substitution local to
+//     each lane, backward substitution by one all-lane reduction per row
+//     (DPP + permlane swaps); cone ops per cone; G'v with a lane per column,
+//     Gv with a lane per row.
 #include <hip/hip_runtime.h>
 
 #include "socp_sqr.hpp"
@@ -23,11 +28,8 @@ namespace socp {
 
 namespace {
 
-__device__ inline double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+// every lane gets the sum over the wavefront (DPP row rotations + row swaps)
+__device__ inline double wave_sum(double v) { return cone_allreduce_rows<false>(v, 4); }
 
 // orders one wavefront's LDS accesses across lanes (and stops the compiler
 // from moving them across this point)
@@ -43,17 +45,30 @@ __device__ inline double bcast(double v, int j) {
   return __hiloint2double(hi, lo);
 }
 
+#ifdef SOCP_DIAG
+// per-phase shader-clock totals of the setup kernel (thread 0 of each
+// workgroup, after the phase's barrier), summed over the batch
+#define SQ_STAMP(i)                                                      \
+  do {                                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                   \
+    if (C.lane == 0 && C.a.stamps) atomicAdd(C.a.stamps + (i), t_ - st_last); \
+    st_last = t_;                                                        \
+  } while (0)
+#else
+#define SQ_STAMP(i) do {} while (0)
+#endif
+
 struct Ctx {
   const SqrArgs& a;
   const SqrLayout& L;
   double* lds;
-  int tid, lane, wave;
+  int lane;
 };
 
 // ------------------------------------------------------------- cone ops
 // scale! (inv = false) / iscale! (inv = true) of one cone (scalings.jl:112-157)
 // by one wavefront; op may alias x (every element is read before it is written).
-__device__ void cone_scale(const double* wb, double mu, const double* x, double* op, int o, int d,
+__device__ __forceinline__ void cone_scale(const double* wb, double mu, const double* x, double* op, int o, int d,
                            int kind, bool inv, int lane) {
   wsync();
   if (kind == POC_K) {
@@ -78,7 +93,7 @@ __device__ void cone_scale(const double* wb, double mu, const double* x, double*
 }
 
 // iprod! (vectors.jl:99-125): t = lam^-1 o v of one cone, closed form of the O(d^2) loop
-__device__ void cone_iprod(const double* lam, const double* v, double* t, int o, int d, int kind, int lane) {
+__device__ __forceinline__ void cone_iprod(const double* lam, const double* v, double* t, int o, int d, int kind, int lane) {
   wsync();
   if (kind == POC_K) {
     for (int i = o + lane; i < o + d; i += 64) t[i] = v[i] / lam[i];
@@ -100,7 +115,7 @@ __device__ void cone_iprod(const double* lam, const double* v, double* t, int o,
 
 // ------------------------------------------------------------ scaling
 // compute_scaling(::SqrScaling) (sqrscalings.jl:50-58, 66-139) of cone c
-__device__ void sqr_scaling_cone(Ctx& C, int c) {
+__device__ __forceinline__ void sqr_scaling_cone(Ctx& C, int c) {
   const SqrLayout& L = C.L;
   double* lds = C.lds;
   const int kind = C.a.cones.kind[c], o = C.a.cones.offs[c], d = C.a.cones.dim[c];
@@ -182,185 +197,259 @@ __device__ void sqr_scaling_cone(Ctx& C, int c) {
   if (bad) lds[L.o_flag] = (double)SQR_DOMAIN;
 }
 
-// ------------------------------------------------------------ Cholesky
-// Right-looking L L' of the lower triangle of M (column-major, leading
-// dimension ld, order n) by the whole workgroup.  The diagonal goes to dg[]
-// (M's own diagonal entries are left stale).  Returns false at a pivot <= 0 or
-// NaN (cholesky! throws PosDefException there).
-__device__ bool chol_wg(Ctx& C, double* M, int ld, int n, double* dg) {
-  for (int j = 0; j < n; ++j) {
-    const double djj = M[j * ld + j];
-    if (!(djj > 0.0)) return false;  // uniform: every thread read the same value
-    const double r = sqrt(djj), ir = 1.0 / r;
-    __syncthreads();
-    if (C.tid == 0) dg[j] = r;
-    for (int i = j + 1 + C.tid; i < n; i += 256) M[j * ld + i] *= ir;
-    __syncthreads();
-    const int i = C.lane;
-    for (int l = j + 1 + C.wave; l < n; l += 4)
-      if (i >= l && i < n) M[l * ld + i] -= M[j * ld + i] * M[j * ld + l];
-    __syncthreads();
+// ------------------------------------------------------------ factor ops
+// L y = b (forward): lane i holds row i of L in h[], b[i] in b; returns y.
+template <int NC>
+__device__ __forceinline__ double fwd_solve(const double (&h)[NC], double rd, int n, double b, int lane) {
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    if (j < n) {
+      const double yj = bcast(b, j) * bcast(rd, j);
+      if (lane == j) b = yj;
+      if (lane > j) b -= h[j] * yj;
+    }
+  }
+  return b;
+}
+// L' x = y (backward): x_i = (y_i - sum_{j>i} L(j,i) x_j) / L(i,i); lane j
+// holds L(j,i) in h[i] and x_j, so each row is one all-lane reduction.
+template <int NC>
+__device__ __forceinline__ double bwd_solve(const double (&h)[NC], double rd, int n, double y, int lane) {
+#pragma unroll
+  for (int i = NC - 1; i >= 0; --i) {
+    if (i < n) {
+      const double s = wave_sum(lane > i && lane < n ? h[i] * y : 0.0);
+      const double xi = (bcast(y, i) - s) * bcast(rd, i);
+      if (lane == i) y = xi;
+    }
+  }
+  return y;
+}
+
+// one column step of a rank-1 modification L L' + sig w w' (column j):
+// r = sqrt(L_jj^2 + sig w_j^2), c = r / L_jj, s = w_j / L_jj,
+// L_ij = (L_ij + sig s w_i) / c, w_i = c w_i - s L_ij (i > j).  false: r^2 <= 0.
+__device__ __forceinline__ bool mod_step(double& hj, double& w, double& rd, int j, double sig, int lane) {
+  const double ljj = bcast(hj, j), wj = bcast(w, j), il = bcast(rd, j);
+  const double r2 = ljj * ljj + sig * wj * wj;
+  if (!(r2 > 0.0)) return false;
+  const double r = sqrt(r2), ir = 1.0 / r;
+  const double cc = r * il, sn = wj * il, icc = ljj * ir;
+  if (lane == j) {
+    hj = r;
+    rd = ir;
+  } else if (lane > j) {
+    const double lij = (hj + sig * sn * w) * icc;
+    hj = lij;
+    w = cc * w - sn * lij;
   }
   return true;
 }
 
-// forward (L y = b) then backward (L' x = y) solve by one wavefront, b one
-// value per lane (rows), n <= 64
-__device__ double chol_solve_wave(const double* M, int ld, const double* dg, int n, double b, int lane) {
-  for (int j = 0; j < n; ++j) {
-    const double xj = bcast(b, j) / dg[j];
-    if (lane == j) b = xj;
-    if (lane > j && lane < n) b -= M[j * ld + lane] * xj;
+// chol of the m x m lower triangle of Sm (column-major, ld) by one wavefront
+// in LDS (m <= 64: one row per lane); 1/diag -> rdg[]; false at a pivot <= 0
+__device__ __forceinline__ bool chol_lds(double* Sm, int ld, int m, double* rdg, int lane) {
+  for (int j = 0; j < m; ++j) {
+    wsync();
+    const double djj = Sm[j * ld + j];
+    if (!(djj > 0.0)) return false;
+    const double r = sqrt(djj), ir = 1.0 / r;
+    if (lane == j) {
+      Sm[j * ld + j] = r;
+      rdg[j] = ir;
+    }
+    if (lane > j && lane < m) Sm[j * ld + lane] *= ir;
+    wsync();
+    if (lane > j && lane < m) {
+      const double lij = Sm[j * ld + lane];
+      for (int l = j + 1; l <= lane; ++l) Sm[l * ld + lane] -= lij * Sm[j * ld + l];
+    }
   }
-  for (int j = n - 1; j >= 0; --j) {
-    const double xj = bcast(b, j) / dg[j];
+  wsync();
+  return true;
+}
+// S^-1 b by one wavefront against chol_lds's factor; b one value per lane
+__device__ __forceinline__ double chol_solve_lds(const double* Sm, int ld, const double* rdg, int m, double b, int lane) {
+  for (int j = 0; j < m; ++j) {
+    const double xj = bcast(b, j) * rdg[j];
     if (lane == j) b = xj;
-    if (lane < j) b -= M[lane * ld + j] * xj;
+    if (lane > j && lane < m) b -= Sm[j * ld + lane] * xj;
+  }
+  for (int j = m - 1; j >= 0; --j) {
+    const double xj = bcast(b, j) * rdg[j];
+    if (lane == j) b = xj;
+    if (lane < j) b -= Sm[lane * ld + j] * xj;
   }
   return b;
 }
 
 // -------------------------------------------------------- setup kernel
-__device__ void setup_problem(Ctx& C, int64_t p) {
+template <int NC>
+__device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
   const SqrArgs& a = C.a;
   const SqrLayout& L = C.L;
   double* lds = C.lds;
+  const int lane = C.lane;
   const int n = a.n, m = a.m, k = a.k, nc = a.nc;
   const double* G = a.G + p * (int64_t)k * n;
   const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
   const bool sing = a.sing && a.sing[p];
   double* rec = a.rec + p * L.rec;
-  for (int i = C.tid; i < k; i += 256) {
+#ifdef SOCP_DIAG
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
+  for (int i = lane; i < k; i += 64) {
     lds[L.o_s + i] = a.s[p * k + i];
     lds[L.o_z + i] = a.z[p * k + i];
+    lds[L.o_one + i] = 1.0;
   }
-  if (C.tid == 0) lds[L.o_flag] = 0.0;
-  __syncthreads();
-  for (int c = C.wave; c < nc; c += 4) sqr_scaling_cone(C, c);
-  __syncthreads();
+  if (lane == 0) lds[L.o_flag] = 0.0;
+  wsync();
+  for (int c = 0; c < nc; ++c) sqr_scaling_cone(C, c);
+  wsync();
+  SQ_STAMP(0);
   int status = (int)lds[L.o_flag];
+  double h[NC];
+  double rd = 0.0;  // lane j: 1 / L(j,j)
   if (status == 0) {
-    // ---- H = G'DG (+A'A): 4x4 blocks per thread, G row chunks via LDS
-    double* M = lds + L.o_L;
-    const int bi = C.tid >> 4, bj = C.tid & 15;
-    const bool act = 4 * bi < n && 4 * bj < n;
-    double acc[4][4];
+    // ---- H = G'DG (+A'A) on f64 MFMA 16x16x4: the lower 16x16 tiles,
+    // Y rows staged through LDS 8 at a time; then one LDS transpose gives each
+    // lane its row of H (v_mfma_f64_16x16x4: A[i][k] / B[k][j] one f64 per
+    // lane at i, j = lane & 15, k = lane >> 4; D[row][col] at col = lane & 15,
+    // row = (lane >> 4) + 4 v)
+    constexpr int NT = NC / 16;
+    typedef double d4v __attribute__((ext_vector_type(4)));
+    d4v acc[NT * (NT + 1) / 2];
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
-#pragma unroll
-      for (int y = 0; y < 4; ++y) acc[x][y] = 0.0;
+    for (int t = 0; t < NT * (NT + 1) / 2; ++t) acc[t] = d4v{0.0, 0.0, 0.0, 0.0};
     double *Ya = lds + L.o_X, *Yb = Ya + SQR_KC * SQR_NW;
+    // non-sing: (iW G)'(iW G) (spsolver.jl:62-64); sing: G'(iWiW G) + A'A (:67-71)
     const double *fa = lds + (sing ? L.o_one : L.o_iW), *fb = lds + (sing ? L.o_D : L.o_iW);
-    if (sing)
-      for (int i = C.tid; i < k; i += 256) lds[L.o_one + i] = 1.0;
-    for (int r0 = 0; r0 < k; r0 += SQR_KC) {
-      __syncthreads();
-      for (int e = C.tid; e < SQR_KC * 64; e += 256) {
-        const int col = e / SQR_KC, r = e % SQR_KC;
-        double g = 0.0, ga = 0.0, gb = 0.0;
-        if (col < n && r0 + r < k) {
-          g = G[(int64_t)col * k + r0 + r];
-          ga = fa[r0 + r] * g;
-          gb = fb[r0 + r] * g;
+    for (int pass = 0; pass < (sing && m > 0 ? 2 : 1); ++pass) {
+      const double* src = pass ? A : G;
+      const int rows = pass ? m : k;
+      for (int r0 = 0; r0 < rows; r0 += SQR_KC) {
+        wsync();
+        for (int e = lane; e < SQR_KC * NC; e += 64) {
+          const int col = e / SQR_KC, r = e % SQR_KC;
+          double g = 0.0;
+          if (col < n && r0 + r < rows) g = src[(int64_t)col * rows + r0 + r];
+          Ya[r * SQR_NW + col] = pass ? g : fa[r0 + r] * g;
+          Yb[r * SQR_NW + col] = pass ? g : fb[r0 + r] * g;
         }
-        Ya[r * SQR_NW + col] = sing ? g : ga;
-        Yb[r * SQR_NW + col] = gb;
-      }
-      __syncthreads();
-      if (act) {
-        const int rn = k - r0 < SQR_KC ? k - r0 : SQR_KC;
-        for (int r = 0; r < rn; ++r) {
-          double va[4], vb[4];
+        wsync();
 #pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            va[x] = Ya[r * SQR_NW + 4 * bi + x];
-            vb[x] = Yb[r * SQR_NW + 4 * bj + x];
+        for (int s = 0; s < SQR_KC; s += 4) {
+          const int rr = s + (lane >> 4), cc = lane & 15;
+          double av[NT], bv[NT];
+#pragma unroll
+          for (int I = 0; I < NT; ++I) {
+            av[I] = Ya[rr * SQR_NW + 16 * I + cc];
+            bv[I] = Yb[rr * SQR_NW + 16 * I + cc];
           }
+          int t = 0;
 #pragma unroll
-          for (int x = 0; x < 4; ++x)
+          for (int I = 0; I < NT; ++I)
 #pragma unroll
-            for (int y = 0; y < 4; ++y) acc[x][y] += va[x] * vb[y];
+            for (int J = 0; J <= I; ++J, ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], bv[J], acc[t], 0, 0, 0);
         }
       }
     }
-    if (act) {
+    {
+      double* T = lds + L.o_X;  // 64 x 17 staging of one 16-column block
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
+      for (int J = 0; J < NT; ++J) {
+        wsync();
 #pragma unroll
-        for (int y = 0; y < 4; ++y) {
-          const int i = 4 * bi + x, j = 4 * bj + y;
-          if (i < n && j < n && i >= j) {
-            double h = acc[x][y];
-            if (sing) {
-              double aa = 0.0;
-              for (int r = 0; r < m; ++r) aa += A[(int64_t)i * m + r] * A[(int64_t)j * m + r];
-              h += aa;
-            }
-            M[j * L.ldl + i] = h;
+        for (int I = 0; I < NT; ++I)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int row = 16 * I + (lane >> 4) + 4 * v;
+            T[row * 17 + (lane & 15)] = I >= J ? acc[I * (I + 1) / 2 + (I >= J ? J : 0)][v] : 0.0;
           }
-        }
+        wsync();
+#pragma unroll
+        for (int c = 0; c < 16; ++c) h[16 * J + c] = T[lane * 17 + c];
+      }
     }
-    __syncthreads();
-    double* dg = lds + L.o_dg;
-    if (!chol_wg(C, M, L.ldl, n, dg)) status = SQR_CHOL_H;
-    // ---- modify_factors! (sqrscalings.jl:160-194)
+    SQ_STAMP(1);
+    // ---- Cholesky, right-looking, in registers
+    bool okc = true;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      if (okc && j < n) {
+        const double d = bcast(h[j], j);
+        okc = d > 0.0;
+        const double r = sqrt(d), ir = 1.0 / r;
+        if (lane == j) {
+          h[j] = r;
+          rd = ir;
+        } else if (lane > j) {
+          h[j] *= ir;
+        } else {
+          h[j] = 0.0;
+        }
+#pragma unroll
+        for (int l = j + 1; l < NC; ++l)
+          if (l < n) h[l] -= h[j] * bcast(h[j], l);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep each column's readlanes with their FMAs
+    }
+    if (!okc) status = SQR_CHOL_H;
+    SQ_STAMP(2);
+    // ---- modify_factors! (sqrscalings.jl:160-194): per SOC cone the update
+    // with G'u, then the downdate with G'v, run as two chains one column apart
     for (int c = 0; c < nc && status == 0; ++c) {
       if (a.cones.kind[c] != SOC_K) continue;
       const int o = a.cones.offs[c], d = a.cones.dim[c];
-      __syncthreads();
-      if (C.tid < 128) {
-        const int sel = C.tid >> 6, i = C.tid & 63;
-        const double* uv = lds + (sel ? L.o_v : L.o_u);
-        double w = 0.0;
-        if (i < n)
-          for (int r = o; r < o + d; ++r) w += G[(int64_t)i * k + r] * uv[r];
-        lds[L.o_w + sel * 64 + i] = w;
-      }
-      __syncthreads();
-      if (C.wave == 0) {
-        bool ok = true;
-        for (int sel = 0; sel < 2 && ok; ++sel) {
-          const double sig = sel ? -1.0 : 1.0;
-          double w = lds[L.o_w + sel * 64 + C.lane];
-          for (int j = 0; j < n; ++j) {
-            const double ljj = dg[j], wj = bcast(w, j);
-            const double r2 = ljj * ljj + sig * wj * wj;
-            if (!(r2 > 0.0)) {
-              ok = false;
-              break;
-            }
-            const double r = sqrt(r2);
-            const double cc = r / ljj, sn = wj / ljj;
-            if (C.lane == j) dg[j] = r;
-            if (C.lane > j && C.lane < n) {
-              const double lij = (M[j * L.ldl + C.lane] + sig * sn * w) / cc;
-              M[j * L.ldl + C.lane] = lij;
-              w = cc * w - sn * lij;
-            }
-          }
-          wsync();
+      double wu = 0.0, wv = 0.0;
+      if (lane < n)
+        for (int r = o; r < o + d; ++r) {
+          const double g = G[(int64_t)lane * k + r];
+          wu += g * lds[L.o_u + r];
+          wv += g * lds[L.o_v + r];
         }
-        if (!ok && C.lane == 0) lds[L.o_flag] = (double)SQR_CHOL_H;
+      bool ok = true;
+#pragma unroll
+      for (int t = 0; t <= NC; ++t) {
+        if (t < NC) {
+          if (ok && t < n) ok = mod_step(h[t], wu, rd, t, 1.0, lane);
+        }
+        if (t >= 1) {
+          if (ok && t - 1 < n) ok = mod_step(h[t - 1], wv, rd, t - 1, -1.0, lane);
+        }
       }
-      __syncthreads();
-      status = (int)lds[L.o_flag];
+      if (!ok) status = SQR_CHOL_H;
     }
-    // ---- C = L^-1 A' (m right-hand sides), S = C'C, chol(S)
+    SQ_STAMP(3);
+    // ---- C = L^-1 A' (four right-hand sides per sweep), S = C'C, chol(S)
     if (status == 0 && m > 0) {
       double* Cm = lds + L.o_X;  // the chunk buffers are free now
-      __syncthreads();
-      for (int q = C.wave; q < m; q += 4) {
-        double b = C.lane < n ? A[(int64_t)C.lane * m + q] : 0.0;
-        for (int j = 0; j < n; ++j) {
-          const double xj = bcast(b, j) / dg[j];
-          if (C.lane == j) b = xj;
-          if (C.lane > j && C.lane < n) b -= M[j * L.ldl + C.lane] * xj;
+      for (int q0 = 0; q0 < m; q0 += 4) {
+        double b[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) b[t] = (q0 + t < m && lane < n) ? A[(int64_t)lane * m + q0 + t] : 0.0;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+          if (j < n) {
+            const double rj = bcast(rd, j);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const double xj = bcast(b[t], j) * rj;
+              if (lane == j) b[t] = xj;
+              if (lane > j) b[t] -= h[j] * xj;
+            }
+          }
         }
-        if (C.lane < n) Cm[q * L.ldl + C.lane] = b;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (q0 + t < m && lane < n) Cm[(q0 + t) * L.ldl + lane] = b[t];
       }
-      __syncthreads();
+      wsync();
+      SQ_STAMP(4);
       double* Sm = lds + L.o_S;
-      for (int e = C.tid; e < m * m; e += 256) {
+      // one entry (r, q), r >= q, per lane: independent dot products
+      for (int e = lane; e < m * m; e += 64) {
         const int r = e % m, q = e / m;
         if (r >= q) {
           double s = 0.0;
@@ -368,40 +457,41 @@ __device__ void setup_problem(Ctx& C, int64_t p) {
           Sm[q * L.ldm + r] = s;
         }
       }
-      __syncthreads();
-      if (!chol_wg(C, Sm, L.ldm, m, lds + L.o_dgs)) status = SQR_CHOL_S;
+      if (!chol_lds(Sm, L.ldm, m, lds + L.o_rdgs, lane)) status = SQR_CHOL_S;
+      SQ_STAMP(5);
     }
   }
-  __syncthreads();
   // ---- the factor record
   if (status == 0) {
-    const double* M = lds + L.o_L;
-    for (int e = C.tid; e < n * n; e += 256) {
-      const int i = e % n, j = e / n;
-      rec[L.r_L + e] = i > j ? M[j * L.ldl + i] : (i == j ? lds[L.o_dg + j] : 0.0);
-    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+      if (j < n && lane < n) rec[L.r_L + j * n + lane] = lane >= j ? h[j] : 0.0;
+    wsync();
     const double* Sm = lds + L.o_S;
-    for (int e = C.tid; e < m * m; e += 256) {
+    for (int e = lane; e < m * m; e += 64) {
       const int i = e % m, j = e / m;
-      rec[L.r_S + e] = i > j ? Sm[j * L.ldm + i] : (i == j ? lds[L.o_dgs + j] : 0.0);
+      rec[L.r_S + e] = i >= j ? Sm[j * L.ldm + i] : 0.0;
     }
-    for (int i = C.tid; i < k; i += 256) {
+    for (int i = lane; i < k; i += 64) {
       rec[L.r_l + i] = lds[L.o_l + i];
       rec[L.r_wb + i] = lds[L.o_wb + i];
     }
-    for (int c = C.tid; c < nc; c += 256) rec[L.r_mu + c] = lds[L.o_mu + c];
+    for (int c = lane; c < nc; c += 64) rec[L.r_mu + c] = lds[L.o_mu + c];
   }
-  if (C.tid == 0) {
+  if (lane == 0) {
     rec[L.r_st] = (double)status;
     a.status[p] = status;
   }
+  SQ_STAMP(6);
 }
 
 // -------------------------------------------------------- solve kernel
-__device__ void solve_problem(Ctx& C, int64_t p) {
+template <int NC>
+__device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
   const SqrArgs& a = C.a;
   const SqrLayout& L = C.L;
   double* lds = C.lds;
+  const int lane = C.lane;
   const int n = a.n, m = a.m, k = a.k, nc = a.nc;
   const double* G = a.G + p * (int64_t)k * n;
   const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
@@ -410,144 +500,137 @@ __device__ void solve_problem(Ctx& C, int64_t p) {
   const int status = (int)rec[L.r_st];
   if (status != 0) {
     const double nan = __builtin_nan("");
-    for (int i = C.tid; i < n; i += 256) a.cx[p * n + i] = nan;
-    for (int i = C.tid; i < m; i += 256) a.cy[p * m + i] = nan;
-    for (int i = C.tid; i < k; i += 256) {
+    for (int i = lane; i < n; i += 64) a.cx[p * n + i] = nan;
+    for (int i = lane; i < m; i += 64) a.cy[p * m + i] = nan;
+    for (int i = lane; i < k; i += 64) {
       a.cz[p * k + i] = nan;
       a.cs[p * k + i] = nan;
     }
-    if (C.tid == 0) a.status[p] = status;
+    if (lane == 0) a.status[p] = status;
     return;
   }
-  double *M = lds + L.o_L, *Sm = lds + L.o_S, *dg = lds + L.o_dg, *dgs = lds + L.o_dgs;
-  for (int e = C.tid; e < n * n; e += 256) {
-    const int i = e % n, j = e / n;
-    if (i > j) M[j * L.ldl + i] = rec[L.r_L + e];
-    if (i == j) dg[i] = rec[L.r_L + e];
-  }
-  for (int e = C.tid; e < m * m; e += 256) {
+  double h[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) h[j] = (j < n && lane < n) ? rec[L.r_L + j * n + lane] : 0.0;
+  const double rd = lane < n ? 1.0 / rec[L.r_L + lane * n + lane] : 0.0;
+  double *Sm = lds + L.o_S, *rdgs = lds + L.o_rdgs;
+  for (int e = lane; e < m * m; e += 64) {
     const int i = e % m, j = e / m;
     if (i > j) Sm[j * L.ldm + i] = rec[L.r_S + e];
-    if (i == j) dgs[i] = rec[L.r_S + e];
+    if (i == j) rdgs[i] = 1.0 / rec[L.r_S + e];
   }
   double *lam = lds + L.o_l, *wb = lds + L.o_wb, *mu = lds + L.o_mu;
   double *dz = lds + L.o_s, *ds = lds + L.o_z;  // the setup's s, z slots
   double *k0 = lds + L.o_D, *k1 = lds + L.o_iW, *k2 = lds + L.o_u, *kt = lds + L.o_v;
-  double *nv = lds + L.o_w, *n1 = nv + 64, *mv = lds + L.o_mv;
-  for (int i = C.tid; i < k; i += 256) {
+  double *nv = lds + L.o_nv, *mv = lds + L.o_mv;
+  for (int i = lane; i < k; i += 64) {
     lam[i] = rec[L.r_l + i];
     wb[i] = rec[L.r_wb + i];
     dz[i] = a.dz[p * k + i];
     ds[i] = a.ds[p * k + i];
   }
-  for (int c = C.tid; c < nc; c += 256) mu[c] = rec[L.r_mu + c];
-  __syncthreads();
+  for (int c = lane; c < nc; c += 64) mu[c] = rec[L.r_mu + c];
+  wsync();
   // k0 = lam \ ds; k1 = W k0; k2 = dz - k1; k1 = W^-1 W^-1 k2   (spsolver.jl:90-96)
-  for (int c = C.wave; c < nc; c += 4) {
+  for (int c = 0; c < nc; ++c) {
     const int o = a.cones.offs[c], d = a.cones.dim[c], kd = a.cones.kind[c];
-    cone_iprod(lam, ds, k0, o, d, kd, C.lane);
-    cone_scale(wb, mu[c], k0, k1, o, d, kd, false, C.lane);
-    wsync();
-    for (int i = o + C.lane; i < o + d; i += 64) k2[i] = dz[i] - k1[i];
-    cone_scale(wb, mu[c], k2, k1, o, d, kd, true, C.lane);
-    cone_scale(wb, mu[c], k1, k1, o, d, kd, true, C.lane);
+    cone_iprod(lam, ds, k0, o, d, kd, lane);
+    cone_scale(wb, mu[c], k0, k1, o, d, kd, false, lane);
+    for (int i = o + lane; i < o + d; i += 64) k2[i] = dz[i] - k1[i];
+    cone_scale(wb, mu[c], k2, k1, o, d, kd, true, lane);
+    cone_scale(wb, mu[c], k1, k1, o, d, kd, true, lane);
   }
-  __syncthreads();
-  // n0 = G' k1 + dx (+ A' dy)   (:97-102): one column per wavefront pass
-  for (int col = C.wave; col < n; col += 4) {
-    double part = 0.0;
-    for (int i = C.lane; i < k; i += 64) part += G[(int64_t)col * k + i] * k1[i];
-    double t = wave_sum(part) + a.dx[p * n + col];
-    if (sing) {
-      double s2 = 0.0;
-      for (int r = C.lane; r < m; r += 64) s2 += A[(int64_t)col * m + r] * a.dy[p * m + r];
-      t += wave_sum(s2);
-    }
-    if (C.lane == 0) nv[col] = t;
+  // n0 = G' k1 + dx (+ A' dy)   (:97-102): a lane per column
+  double n0 = 0.0;
+  if (lane < n) {
+    for (int i = 0; i < k; ++i) n0 += G[(int64_t)lane * k + i] * k1[i];
+    n0 += a.dx[p * n + lane];
+    if (sing)
+      for (int r = 0; r < m; ++r) n0 += A[(int64_t)lane * m + r] * a.dy[p * m + r];
   }
-  __syncthreads();
   // n1 = H^-1 n0 (:104-107)
-  if (C.wave == 0) {
-    const double b = chol_solve_wave(M, L.ldl, dg, n, C.lane < n ? nv[C.lane] : 0.0, C.lane);
-    if (C.lane < n) n1[C.lane] = b;
-  }
-  __syncthreads();
+  const double n1 = bwd_solve<NC>(h, rd, n, fwd_solve<NC>(h, rd, n, n0, lane), lane);
   if (m > 0) {
     // m0 = A n1 - dy; cy = S^-1 m0; m0 = sing ? dy - cy : -cy   (:108-118)
-    if (C.wave == 0) {
-      double t = 0.0;
-      if (C.lane < m) {
-        for (int j = 0; j < n; ++j) t += A[(int64_t)j * m + C.lane] * n1[j];
-        t -= a.dy[p * m + C.lane];
-      }
-      const double cy = chol_solve_wave(Sm, L.ldm, dgs, m, t, C.lane);
-      if (C.lane < m) {
-        a.cy[p * m + C.lane] = cy;
-        const double dy = a.dy[p * m + C.lane];
-        mv[C.lane] = sing ? dy - cy : -cy;
-      }
+    if (lane < n) nv[lane] = n1;
+    wsync();
+    double t = 0.0;
+    if (lane < m) {
+      for (int j = 0; j < n; ++j) t += A[(int64_t)j * m + lane] * nv[j];
+      t -= a.dy[p * m + lane];
     }
-    __syncthreads();
+    const double cy = chol_solve_lds(Sm, L.ldm, rdgs, m, t, lane);
+    if (lane < m) {
+      a.cy[p * m + lane] = cy;
+      const double dy = a.dy[p * m + lane];
+      mv[lane] = sing ? dy - cy : -cy;
+    }
+    wsync();
     // n0 += A' m0   (:119-120)
-    for (int j = C.tid; j < n; j += 256) {
-      double t = 0.0;
-      for (int r = 0; r < m; ++r) t += A[(int64_t)j * m + r] * mv[r];
-      nv[j] += t;
-    }
-    __syncthreads();
+    if (lane < n)
+      for (int r = 0; r < m; ++r) n0 += A[(int64_t)lane * m + r] * mv[r];
   }
   // cx = H^-1 n0 (:122-124)
-  if (C.wave == 0) {
-    const double b = chol_solve_wave(M, L.ldl, dg, n, C.lane < n ? nv[C.lane] : 0.0, C.lane);
-    if (C.lane < n) {
-      n1[C.lane] = b;
-      a.cx[p * n + C.lane] = b;
-    }
+  const double cx = bwd_solve<NC>(h, rd, n, fwd_solve<NC>(h, rd, n, n0, lane), lane);
+  if (lane < n) {
+    a.cx[p * n + lane] = cx;
+    nv[lane] = cx;
   }
-  __syncthreads();
-  // k1 = G cx - k2 (:125-126), one row per thread
-  for (int i = C.tid; i < k; i += 256) {
+  wsync();
+  // k1 = G cx - k2 (:125-126), a lane per row
+  for (int i = lane; i < k; i += 64) {
     double t = 0.0;
-    for (int j = 0; j < n; ++j) t += G[(int64_t)j * k + i] * n1[j];
+    for (int j = 0; j < n; ++j) t += G[(int64_t)j * k + i] * nv[j];
     kt[i] = t - k2[i];
   }
-  __syncthreads();
   // cz = W^-1 W^-1 k1; k1 = W cz; k0 -= k1; cs = W k0   (:127-131)
   double *cz = k2, *cs = k1;
-  for (int c = C.wave; c < nc; c += 4) {
+  for (int c = 0; c < nc; ++c) {
     const int o = a.cones.offs[c], d = a.cones.dim[c], kd = a.cones.kind[c];
-    cone_scale(wb, mu[c], kt, cz, o, d, kd, true, C.lane);
-    cone_scale(wb, mu[c], cz, cz, o, d, kd, true, C.lane);
-    cone_scale(wb, mu[c], cz, kt, o, d, kd, false, C.lane);
-    wsync();
-    for (int i = o + C.lane; i < o + d; i += 64) k0[i] -= kt[i];
-    cone_scale(wb, mu[c], k0, cs, o, d, kd, false, C.lane);
+    cone_scale(wb, mu[c], kt, cz, o, d, kd, true, lane);
+    cone_scale(wb, mu[c], cz, cz, o, d, kd, true, lane);
+    cone_scale(wb, mu[c], cz, kt, o, d, kd, false, lane);
+    for (int i = o + lane; i < o + d; i += 64) k0[i] -= kt[i];
+    cone_scale(wb, mu[c], k0, cs, o, d, kd, false, lane);
   }
-  __syncthreads();
-  for (int i = C.tid; i < k; i += 256) {
+  wsync();
+  for (int i = lane; i < k; i += 64) {
     a.cz[p * k + i] = cz[i];
     a.cs[p * k + i] = cs[i];
   }
-  if (C.tid == 0) a.status[p] = 0;
+  if (lane == 0) a.status[p] = 0;
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void socp_sqr_setup_kernel(SqrArgs a) {
+template <int NC>
+__global__ __launch_bounds__(64) void socp_sqr_setup_kernel(SqrArgs a) {
   extern __shared__ double lds_dyn[];
   const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
-  Ctx C{a, L, lds_dyn, (int)threadIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6)};
-  setup_problem(C, (int64_t)blockIdx.x);
+  Ctx C{a, L, lds_dyn, (int)threadIdx.x};
+  setup_problem<NC>(C, (int64_t)blockIdx.x);
 }
 
-__global__ __launch_bounds__(256) void socp_sqr_solve_kernel(SqrArgs a) {
+template <int NC>
+__global__ __launch_bounds__(64) void socp_sqr_solve_kernel(SqrArgs a) {
   extern __shared__ double lds_dyn[];
   const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
-  Ctx C{a, L, lds_dyn, (int)threadIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6)};
-  solve_problem(C, (int64_t)blockIdx.x);
+  Ctx C{a, L, lds_dyn, (int)threadIdx.x};
+  solve_problem<NC>(C, (int64_t)blockIdx.x);
 }
 
-const void* sqr_setup_kernel_ptr() { return (const void*)socp_sqr_setup_kernel; }
-const void* sqr_solve_kernel_ptr() { return (const void*)socp_sqr_solve_kernel; }
+// NC = n rounded up to 16
+const void* sqr_setup_kernel_ptr(int n) {
+  if (n <= 16) return (const void*)socp_sqr_setup_kernel<16>;
+  if (n <= 32) return (const void*)socp_sqr_setup_kernel<32>;
+  if (n <= 48) return (const void*)socp_sqr_setup_kernel<48>;
+  return (const void*)socp_sqr_setup_kernel<64>;
+}
+const void* sqr_solve_kernel_ptr(int n) {
+  if (n <= 16) return (const void*)socp_sqr_solve_kernel<16>;
+  if (n <= 32) return (const void*)socp_sqr_solve_kernel<32>;
+  if (n <= 48) return (const void*)socp_sqr_solve_kernel<48>;
+  return (const void*)socp_sqr_solve_kernel<64>;
+}
 
 }  // namespace socp

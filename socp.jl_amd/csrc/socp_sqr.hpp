@@ -9,15 +9,14 @@ namespace socp {
 
 constexpr int SQR_NMAX = 64;   // n, m <= 64: one row per lane in the triangular solves
 constexpr int SQR_KMAX = 256;  // k
-constexpr int SQR_KC = 16;     // G rows per LDS chunk in the H product
+constexpr int SQR_KC = 8;      // G rows per LDS chunk in the H product
 constexpr int SQR_NW = 66;     // LDS row stride of a chunk (doubles; 16-byte aligned rows)
 constexpr int SQR_CHOL_H = 2, SQR_CHOL_S = 3, SQR_DOMAIN = 4;  // include/socp.h status codes
 
 struct SqrLayout {
-  int ldl, ldm;  // LDS leading dimensions of L_H and L_S (odd: conflict-free row walks)
+  int ldl, ldm;  // LDS leading dimensions of C = L^-1 A' and L_S (odd: conflict-free row walks)
   // LDS offsets (doubles)
-  int o_s, o_z, o_D, o_iW, o_u, o_v, o_l, o_wb, o_one, o_mu, o_dg, o_dgs, o_w, o_mv, o_flag, o_L,
-      o_X, o_S, total;
+  int o_s, o_z, o_D, o_iW, o_u, o_v, o_l, o_wb, o_one, o_mu, o_rdgs, o_nv, o_mv, o_flag, o_X, o_S, total;
   // per-problem factor record (doubles): L_H (n x n, column-major, zeros above
   // the diagonal), L_S (m x m), lambda, wb (k each), mu (nc), status
   int64_t r_L, r_S, r_l, r_wb, r_mu, r_st, rec;
@@ -40,15 +39,15 @@ __host__ __device__ inline SqrLayout sqr_layout(int n, int m, int k, int nc) {
   L.o_wb = o;   o += KP;
   L.o_one = o;  o += KP;
   L.o_mu = o;   o += MAXC;
-  L.o_dg = o;   o += 64;
-  L.o_dgs = o;  o += 64;
-  L.o_w = o;    o += 128;
+  L.o_rdgs = o; o += 64;
+  L.o_nv = o;   o += 64;
   L.o_mv = o;   o += 64;
   L.o_flag = o; o += 2;
-  L.o_L = o;    o += ev(n * L.ldl);
   L.o_X = o;
-  const int chunks = 2 * SQR_KC * SQR_NW, cm = m * L.ldl;
-  o += ev(chunks > cm ? chunks : cm);
+  int xs = 2 * SQR_KC * SQR_NW;          // Y row chunks (H product)
+  if (xs < 64 * 17) xs = 64 * 17;        // the H tile transpose
+  if (xs < m * L.ldl) xs = m * L.ldl;    // C = L^-1 A'
+  o += ev(xs);
   L.o_S = o;    o += ev(m * L.ldm);
   L.total = o;
   int64_t r = 0;
@@ -73,9 +72,10 @@ struct SqrArgs {
   double *cx, *cy, *cz, *cs;        // solve: solutions
   int32_t* status;         // B
   double* rec;             // B x rec
+  unsigned long long* stamps;  // diagnostic build: per-phase cycle totals (setup kernel), else NULL
 };
 
-const void* sqr_setup_kernel_ptr();
-const void* sqr_solve_kernel_ptr();
+const void* sqr_setup_kernel_ptr(int n);  // instantiation for n (rounded up to 16)
+const void* sqr_solve_kernel_ptr(int n);
 
 }  // namespace socp

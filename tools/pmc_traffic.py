@@ -3,13 +3,17 @@ WRITE_SIZE), corrected as /opt/skills/guides/MI355X_MICROARCH.md prescribes for
 gfx950: FETCH_SIZE reports half the bytes of a wide streaming read (x2);
 WRITE_SIZE is taken as reported.  Both counters are in KiB.
 
-usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG BATCH FIXED_K OUT.json
+usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR CONFIG BATCH FIXED_K OUT.json [KERNEL_SUBSTR]
+(KERNEL_SUBSTR: which kernel's dispatches to count; default the solver kernels)
 """
 import csv
 import glob
 import json
 import os
 import sys
+
+
+KERNELS = ("socp_small_kernel", "socp_large_kernel")
 
 
 def per_dispatch(d, counter):
@@ -19,7 +23,7 @@ def per_dispatch(d, counter):
     vals = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if not any(kn in r["Kernel_Name"] for kn in ("socp_small_kernel", "socp_large_kernel")) or r["Counter_Name"] != counter:
+            if not any(kn in r["Kernel_Name"] for kn in KERNELS) or r["Counter_Name"] != counter:
                 continue
             key = (f, r["Dispatch_Id"])
             vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
@@ -29,13 +33,16 @@ def per_dispatch(d, counter):
 
 
 def main():
+    global KERNELS
     fdir, wdir, cfg, batch, fk, out = sys.argv[1:7]
+    if len(sys.argv) > 7:
+        KERNELS = (sys.argv[7],)
     fetch = per_dispatch(fdir, "FETCH_SIZE")
     write = per_dispatch(wdir, "WRITE_SIZE")
     f_kib = fetch[len(fetch) // 2]
     w_kib = write[len(write) // 2]
     res = {
-        "config": cfg, "batch": int(batch), "fixed_k": int(fk),
+        "config": cfg, "batch": int(batch), "fixed_k": int(fk), "kernels": list(KERNELS),
         "fetch_size_kib_raw": f_kib, "write_size_kib_raw": w_kib,
         "hbm_read_bytes": 2.0 * f_kib * 1024.0,
         "hbm_write_bytes": w_kib * 1024.0,
