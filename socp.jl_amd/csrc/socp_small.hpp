@@ -525,7 +525,10 @@ struct Small {
     // across, so the loads are issued in batches of 16 into VGPRs first (one
     // HBM round trip per batch, not per element).  Padding (row >= k or
     // col >= n) reads element 0 and is zeroed with an integer mask.
-    constexpr int GT = NP * NQ, GB = 16;
+#ifndef SOCP_GLOAD_BATCH
+#define SOCP_GLOAD_BATCH 16
+#endif
+    constexpr int GT = NP * NQ, GB = SOCP_GLOAD_BATCH;
 #pragma unroll
     for (int b0 = 0; b0 < GT; b0 += GB) {
       uint64_t tmp[GB];
