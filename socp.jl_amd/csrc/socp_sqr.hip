@@ -393,48 +393,58 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
         for (int l = j + 1; l < NC; ++l)
           if (l < n) h[l] -= h[j] * bcast(h[j], l);
       }
-      __builtin_amdgcn_sched_barrier(0);  // keep each column's readlanes with their FMAs
     }
     if (!okc) status = SQR_CHOL_H;
     SQ_STAMP(2);
     // ---- modify_factors! (sqrscalings.jl:160-194): per SOC cone the update
-    // with G'u, then the downdate with G'v, run as two chains one column apart
-    for (int c = 0; c < nc && status == 0; ++c) {
-      if (a.cones.kind[c] != SOC_K) continue;
-      const int o = a.cones.offs[c], d = a.cones.dim[c];
-      double wu = 0.0, wv = 0.0;
-      if (lane < n)
-        for (int r = o; r < o + d; ++r) {
-          const double g = G[(int64_t)lane * k + r];
-          wu += g * lds[L.o_u + r];
-          wv += g * lds[L.o_v + r];
+    // with G'u, then the downdate with G'v.  Two cones per sweep as four
+    // chains one column apart (u1, v1, u2, v2): each column is final for the
+    // earlier chains when a later one reaches it, so the result is the
+    // sequential one bit for bit, and the four latency chains overlap.  The
+    // SOC cones follow the POC cones (check_problem).
+    int c0 = 0;
+    while (c0 < nc && a.cones.kind[c0] != SOC_K) ++c0;
+    for (; c0 < nc && status == 0; c0 += 2) {
+      const int nch = c0 + 1 < nc ? 4 : 2;
+      double w[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (lane < n && 2 * q < nch) {
+          const int o = a.cones.offs[c0 + q], d = a.cones.dim[c0 + q];
+          for (int r = o; r < o + d; ++r) {
+            const double g = G[(int64_t)lane * k + r];
+            w[2 * q] += g * lds[L.o_u + r];
+            w[2 * q + 1] += g * lds[L.o_v + r];
+          }
         }
+      }
       bool ok = true;
 #pragma unroll
-      for (int t = 0; t <= NC; ++t) {
-        if (t < NC) {
-          if (ok && t < n) ok = mod_step(h[t], wu, rd, t, 1.0, lane);
-        }
-        if (t >= 1) {
-          if (ok && t - 1 < n) ok = mod_step(h[t - 1], wv, rd, t - 1, -1.0, lane);
+      for (int t = 0; t < NC + 3; ++t) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int j = t - c;
+          if (j >= 0 && j < NC) {
+            if (ok && c < nch && j < n) ok = mod_step(h[j], w[c], rd, j, (c & 1) ? -1.0 : 1.0, lane);
+          }
         }
       }
       if (!ok) status = SQR_CHOL_H;
     }
     SQ_STAMP(3);
-    // ---- C = L^-1 A' (four right-hand sides per sweep), S = C'C, chol(S)
+    // ---- C = L^-1 A' (SQR_RHS right-hand sides per sweep), S = C'C, chol(S)
     if (status == 0 && m > 0) {
       double* Cm = lds + L.o_X;  // the chunk buffers are free now
-      for (int q0 = 0; q0 < m; q0 += 4) {
-        double b[4];
+      for (int q0 = 0; q0 < m; q0 += SQR_RHS) {
+        double b[SQR_RHS];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) b[t] = (q0 + t < m && lane < n) ? A[(int64_t)lane * m + q0 + t] : 0.0;
+        for (int t = 0; t < SQR_RHS; ++t) b[t] = (q0 + t < m && lane < n) ? A[(int64_t)lane * m + q0 + t] : 0.0;
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
           if (j < n) {
             const double rj = bcast(rd, j);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < SQR_RHS; ++t) {
               const double xj = bcast(b[t], j) * rj;
               if (lane == j) b[t] = xj;
               if (lane > j) b[t] -= h[j] * xj;
@@ -442,7 +452,7 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
           }
         }
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < SQR_RHS; ++t)
           if (q0 + t < m && lane < n) Cm[(q0 + t) * L.ldl + lane] = b[t];
       }
       wsync();

@@ -11,6 +11,7 @@ constexpr int SQR_NMAX = 64;   // n, m <= 64: one row per lane in the triangular
 constexpr int SQR_KMAX = 256;  // k
 constexpr int SQR_KC = 8;      // G rows per LDS chunk in the H product
 constexpr int SQR_NW = 66;     // LDS row stride of a chunk (doubles; 16-byte aligned rows)
+constexpr int SQR_RHS = 8;     // right-hand sides per forward sweep in L^-1 A'
 constexpr int SQR_CHOL_H = 2, SQR_CHOL_S = 3, SQR_DOMAIN = 4;  // include/socp.h status codes
 
 struct SqrLayout {
