@@ -203,11 +203,10 @@ template <int NC>
 __device__ __forceinline__ double fwd_solve(const double (&h)[NC], double rd, int n, double b, int lane) {
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
-    if (j < n) {
-      const double yj = bcast(b, j) * bcast(rd, j);
-      if (lane == j) b = yj;
-      if (lane > j) b -= h[j] * yj;
-    }
+    const double yj = bcast(b, j) * bcast(rd, j);
+    if (lane == j) b = yj;
+    if (lane > j) b -= h[j] * yj;
+    __builtin_amdgcn_sched_barrier(0);
   }
   return b;
 }
@@ -217,11 +216,10 @@ template <int NC>
 __device__ __forceinline__ double bwd_solve(const double (&h)[NC], double rd, int n, double y, int lane) {
 #pragma unroll
   for (int i = NC - 1; i >= 0; --i) {
-    if (i < n) {
-      const double s = wave_sum(lane > i && lane < n ? h[i] * y : 0.0);
-      const double xi = (bcast(y, i) - s) * bcast(rd, i);
-      if (lane == i) y = xi;
-    }
+    const double s = wave_sum(lane > i ? h[i] * y : 0.0);
+    const double xi = (bcast(y, i) - s) * bcast(rd, i);
+    if (lane == i) y = xi;
+    __builtin_amdgcn_sched_barrier(0);
   }
   return y;
 }
@@ -232,7 +230,6 @@ __device__ __forceinline__ double bwd_solve(const double (&h)[NC], double rd, in
 __device__ __forceinline__ bool mod_step(double& hj, double& w, double& rd, int j, double sig, int lane) {
   const double ljj = bcast(hj, j), wj = bcast(w, j), il = bcast(rd, j);
   const double r2 = ljj * ljj + sig * wj * wj;
-  if (!(r2 > 0.0)) return false;
   const double r = sqrt(r2), ir = 1.0 / r;
   const double cc = r * il, sn = wj * il, icc = ljj * ir;
   if (lane == j) {
@@ -243,7 +240,7 @@ __device__ __forceinline__ bool mod_step(double& hj, double& w, double& rd, int 
     hj = lij;
     w = cc * w - sn * lij;
   }
-  return true;
+  return r2 > 0.0;
 }
 
 // chol of the m x m lower triangle of Sm (column-major, ld) by one wavefront
@@ -310,7 +307,7 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
   SQ_STAMP(0);
   int status = (int)lds[L.o_flag];
   double h[NC];
-  double rd = 0.0;  // lane j: 1 / L(j,j)
+  double rd = lane >= n ? 1.0 : 0.0;  // lane j: 1 / L(j,j) (1 on the identity-padded rows)
   if (status == 0) {
     // ---- H = G'DG (+A'A) on f64 MFMA 16x16x4: the lower 16x16 tiles,
     // Y rows staged through LDS 8 at a time; then one LDS transpose gives each
@@ -372,29 +369,34 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
         for (int c = 0; c < 16; ++c) h[16 * J + c] = T[lane * 17 + c];
       }
     }
+    // rows n..NC-1 become identity rows: the padded factor is [L 0; 0 I], so
+    // the unrolled column loops below need no `j < n` guards (zero-padded G
+    // columns leave rows < n with zeros there)
+#pragma unroll
+    for (int l = 0; l < NC; ++l)
+      if (lane >= n) h[l] = lane == l ? 1.0 : 0.0;
     SQ_STAMP(1);
     // ---- Cholesky, right-looking, in registers
-    bool okc = true;
+    bool badc = false;  // a pivot <= 0 or NaN: the rest runs on NaNs, the status says so
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-      if (okc && j < n) {
-        const double d = bcast(h[j], j);
-        okc = d > 0.0;
-        const double r = sqrt(d), ir = 1.0 / r;
-        if (lane == j) {
-          h[j] = r;
-          rd = ir;
-        } else if (lane > j) {
-          h[j] *= ir;
-        } else {
-          h[j] = 0.0;
-        }
-#pragma unroll
-        for (int l = j + 1; l < NC; ++l)
-          if (l < n) h[l] -= h[j] * bcast(h[j], l);
+      if (j >= n) continue;  // one uniform branch per column (the padded pivots are 1)
+      const double d = bcast(h[j], j);
+      badc |= !(d > 0.0);
+      const double r = sqrt(d), ir = 1.0 / r;
+      if (lane == j) {
+        h[j] = r;
+        rd = ir;
+      } else if (lane > j) {
+        h[j] *= ir;
+      } else {
+        h[j] = 0.0;
       }
+#pragma unroll
+      for (int l = j + 1; l < NC; ++l) h[l] -= h[j] * bcast(h[j], l);
+      __builtin_amdgcn_sched_barrier(0);  // bounds the live ranges of straight-line code
     }
-    if (!okc) status = SQR_CHOL_H;
+    if (badc) status = SQR_CHOL_H;
     SQ_STAMP(2);
     // ---- modify_factors! (sqrscalings.jl:160-194): per SOC cone the update
     // with G'u, then the downdate with G'v.  Two cones per sweep as four
@@ -418,18 +420,17 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
           }
         }
       }
-      bool ok = true;
+      bool bad = false;
 #pragma unroll
       for (int t = 0; t < NC + 3; ++t) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int j = t - c;
-          if (j >= 0 && j < NC) {
-            if (ok && c < nch && j < n) ok = mod_step(h[j], w[c], rd, j, (c & 1) ? -1.0 : 1.0, lane);
-          }
+          if (j >= 0 && j < NC && (c < 2 || nch == 4)) bad |= !mod_step(h[j], w[c], rd, j, (c & 1) ? -1.0 : 1.0, lane);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if (!ok) status = SQR_CHOL_H;
+      if (bad) status = SQR_CHOL_H;
     }
     SQ_STAMP(3);
     // ---- C = L^-1 A' (SQR_RHS right-hand sides per sweep), S = C'C, chol(S)
@@ -441,15 +442,14 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
         for (int t = 0; t < SQR_RHS; ++t) b[t] = (q0 + t < m && lane < n) ? A[(int64_t)lane * m + q0 + t] : 0.0;
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-          if (j < n) {
-            const double rj = bcast(rd, j);
+          const double rj = bcast(rd, j);
 #pragma unroll
-            for (int t = 0; t < SQR_RHS; ++t) {
-              const double xj = bcast(b[t], j) * rj;
-              if (lane == j) b[t] = xj;
-              if (lane > j) b[t] -= h[j] * xj;
-            }
+          for (int t = 0; t < SQR_RHS; ++t) {
+            const double xj = bcast(b[t], j) * rj;
+            if (lane == j) b[t] = xj;
+            if (lane > j) b[t] -= h[j] * xj;
           }
+          __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int t = 0; t < SQR_RHS; ++t)
@@ -520,9 +520,10 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
     return;
   }
   double h[NC];
+  // rows n..NC-1 as identity rows ([L 0; 0 I]): no guards in the solves
 #pragma unroll
-  for (int j = 0; j < NC; ++j) h[j] = (j < n && lane < n) ? rec[L.r_L + j * n + lane] : 0.0;
-  const double rd = lane < n ? 1.0 / rec[L.r_L + lane * n + lane] : 0.0;
+  for (int j = 0; j < NC; ++j) h[j] = (j < n && lane < n) ? rec[L.r_L + j * n + lane] : (lane == j ? 1.0 : 0.0);
+  const double rd = lane < n ? 1.0 / rec[L.r_L + lane * n + lane] : 1.0;
   double *Sm = lds + L.o_S, *rdgs = lds + L.o_rdgs;
   for (int e = lane; e < m * m; e += 64) {
     const int i = e % m, j = e / m;
@@ -614,7 +615,7 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
 }  // namespace
 
 template <int NC>
-__global__ __launch_bounds__(64) void socp_sqr_setup_kernel(SqrArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void socp_sqr_setup_kernel(SqrArgs a) {
   extern __shared__ double lds_dyn[];
   const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
   Ctx C{a, L, lds_dyn, (int)threadIdx.x};
