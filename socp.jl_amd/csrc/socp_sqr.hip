@@ -322,17 +322,32 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
     double *Ya = lds + L.o_X, *Yb = Ya + SQR_KC * SQR_NW;
     // non-sing: (iW G)'(iW G) (spsolver.jl:62-64); sing: G'(iWiW G) + A'A (:67-71)
     const double *fa = lds + (sing ? L.o_one : L.o_iW), *fb = lds + (sing ? L.o_D : L.o_iW);
+    constexpr int PE = SQR_KC * NC / 64;  // chunk elements per lane
     for (int pass = 0; pass < (sing && m > 0 ? 2 : 1); ++pass) {
       const double* src = pass ? A : G;
       const int rows = pass ? m : k;
+      // software-pipelined: chunk r0 + KC is loaded while chunk r0 is used
+      double gn[PE];
+#pragma unroll
+      for (int q = 0; q < PE; ++q) {
+        const int e = lane + 64 * q, col = e / SQR_KC, r = e % SQR_KC;
+        gn[q] = (col < n && r < rows) ? src[(int64_t)col * rows + r] : 0.0;
+      }
       for (int r0 = 0; r0 < rows; r0 += SQR_KC) {
         wsync();
-        for (int e = lane; e < SQR_KC * NC; e += 64) {
-          const int col = e / SQR_KC, r = e % SQR_KC;
-          double g = 0.0;
-          if (col < n && r0 + r < rows) g = src[(int64_t)col * rows + r0 + r];
-          Ya[r * SQR_NW + col] = pass ? g : fa[r0 + r] * g;
-          Yb[r * SQR_NW + col] = pass ? g : fb[r0 + r] * g;
+#pragma unroll
+        for (int q = 0; q < PE; ++q) {
+          const int e = lane + 64 * q, col = e / SQR_KC, r = e % SQR_KC;
+          const double g = gn[q];
+          const bool in = r0 + r < rows;
+          Ya[r * SQR_NW + col] = pass ? g : (in ? fa[r0 + r] * g : 0.0);
+          Yb[r * SQR_NW + col] = pass ? g : (in ? fb[r0 + r] * g : 0.0);
+        }
+#pragma unroll
+        for (int q = 0; q < PE; ++q) {  // the next chunk's loads fly under this chunk's MFMAs
+          const int e = lane + 64 * q, col = e / SQR_KC, r = e % SQR_KC;
+          const int rn = r0 + SQR_KC + r;
+          gn[q] = (col < n && rn < rows) ? src[(int64_t)col * rows + rn] : 0.0;
         }
         wsync();
 #pragma unroll
