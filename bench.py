@@ -221,7 +221,7 @@ def sqr_model(n, m, k, cones):
     return f_setup, f_solve, b_setup, b_solve
 
 
-def sqr_bench(args):
+def sqr_bench(args, emit=True):
     """--mode sqr: the rank-update plugin (socp_sqr_*, SparseSolver + SqrScaling,
     spsolver.jl / sqrscalings.jl) at the config's shape.  A step = setup_iter +
     two solve_kkt (one IPM iteration's KKT work) over the whole batch, device
@@ -323,7 +323,9 @@ def sqr_bench(args):
                                 "sample": f"median of 3 reps x {chunk} {cfg.name} problems, fixed-K={cfg.fixed_k}, "
                                           "oracle F_SQR (SqrScaling + rank-update factor restated, whole IPM "
                                           "iteration: a superset of the KKT work timed on the GPU)"}
-    print(json.dumps(line), flush=True)
+    if emit:
+        print(json.dumps(line), flush=True)
+    return line
 
 
 def main():
@@ -476,6 +478,14 @@ def main():
         }
         if world == 1 and not args.no_ingest:
             line["ingest"] = ingest_line(S, cfg, B, K, tol, (c, A, b, G, h), args.steps, ctx)
+        if world == 1 and not args.no_ingest and cfg.name == "C2" and not ref_rule:
+            # the rank-update plugin (SparseSolver + SqrScaling, socp_sqr_*) at the same shape: its
+            # own line is `--mode sqr`; summarised here so every default run records it
+            sq = sqr_bench(argparse.Namespace(config=cfg.name, batch=B, steps=args.steps, warmup=1, no_cpu=True,
+                                              traffic_json=None), emit=False)
+            line["rank_update_plugin"] = {"value": sq["value"], "unit": sq["unit"], "ms_per_step": sq["ms_per_step"],
+                                          "kernels_ms": sq["kernels"], "status_counts": sq["status_counts"],
+                                          "mode": "bench.py --mode sqr (setup_iter + 2 x solve_kkt per problem)"}
         if not args.no_cpu and world == 1:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol)
             line["cpu_baseline_structured"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol,
