@@ -11,6 +11,9 @@ dense factor, so agreement is to rounding, never bitwise):
   * batches at the C1/C2 shapes at interior iterates: HIP vs the oracle's
     rank-update restatement, rel <= 1e-9 where kappa(H) <= 1e5; HIP sqr vs the
     HIP dense plugin at the same tolerance; m = 0 and sing problems;
+  * every instantiation (NC = 16, 32, 48, 64) and the shape limits (m = 64,
+    k = 256, 15 cones, an LP with no SOC cone) vs the oracle, gate
+    max(1e-9, 1e-15 kappa(H) kappa(S));
   * failures (domain error, lost definiteness in a downdate) stay in their
     problem; solve_kkt before setup_iter is refused; per-call H2D bytes.
 """
@@ -220,3 +223,52 @@ def test_sqr_device_tensors_equal_host():
     assert np.array_equal(std.cpu().numpy(), sth)
     for key in ("cx", "cy", "cz", "cs"):
         assert np.array_equal(od[key].cpu().numpy(), oh[key]), key
+
+
+def _interior(rng, cones, B, k):
+    """B interior points of the cone product (POC entries > 0, SOC heads above the tail norm)."""
+    v = np.zeros((B, k))
+    for kind, o, d in cones:
+        if kind == 0:
+            v[:, o:o + d] = rng.uniform(0.3, 2.0, (B, d))
+        else:
+            v[:, o + 1:o + d] = rng.uniform(-0.4, 0.4, (B, d - 1))
+            v[:, o] = np.linalg.norm(v[:, o + 1:o + d], axis=1) + rng.uniform(0.2, 1.0, B)
+    return v
+
+
+@pytest.mark.parametrize("n,m,k,cones", [
+    (40, 8, 60, [(0, 0, 20), (1, 20, 40)]),                     # NC = 48
+    (17, 3, 25, [(1, 0, 5), (1, 5, 9), (1, 14, 11)]),            # NC = 32, ragged, three SOC cones
+    (64, 64, 100, [(0, 0, 36), (1, 36, 64)]),                    # m at its limit, k > 64
+    (9, 0, 12, [(0, 0, 12)]),                                    # LP: no SOC cone, no modification
+    (30, 5, 256, [(0, 0, 16)] + [(1, 16 + 16 * i, 16) for i in range(15)]),  # k at its limit, 15 cones
+])
+def test_sqr_shapes_vs_oracle(oracle, n, m, k, cones):
+    rng = np.random.default_rng(n * 1000 + m * 10 + k)
+    B = 12
+    G = rng.standard_normal((B, k, n))
+    A = rng.standard_normal((B, m, n))
+    s, z = _interior(rng, cones, B, k), _interior(rng, cones, B, k)
+    Gf = np.concatenate([G[p].ravel(order="F") for p in range(B)])
+    Af = np.concatenate([A[p].ravel(order="F") for p in range(B)]) if m else None
+    h = S.SqrHandle(cones, n, m, k, Af, Gf, np.zeros(B, np.uint8))
+    st = h.setup_iter(s.ravel(), z.ravel())
+    r = [rng.standard_normal(B * q) for q in (n, m, k, k)]
+    got = h.solve_kkt(r[0], r[1] if m else None, r[2], r[3])
+    for p in range(B):
+        sl = lambda v, q: v[p * q:(p + 1) * q]  # noqa: E731
+        o = oracle.sqr_kkt_single(cones, A[p], G[p], False, s[p], z[p], sl(r[0], n), sl(r[1], m), sl(r[2], k),
+                                  sl(r[3], k))
+        assert st[p] == o["status"], p
+        if o["status"]:
+            continue
+        assert np.abs(np.tril(h.factor(p)) - o["L"]).max() <= 1e-9 * np.abs(o["L"]).max(), p
+        # rounding-level agreement, scaled by the conditioning of H and S = A H^-1 A'
+        Hm = o["L"] @ o["L"].T
+        kap = np.linalg.cond(Hm) * (np.linalg.cond(A[p] @ np.linalg.solve(Hm, A[p].T)) if m else 1.0)
+        tol = max(1e-9, 1e-15 * kap)
+        for key, q in (("cx", n), ("cy", m), ("cz", k), ("cs", k)):
+            if q:
+                ref = o[key]
+                assert np.abs(sl(got[key], q) - ref).max() <= tol * max(1.0, np.abs(ref).max()), (p, key, kap)
