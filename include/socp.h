@@ -207,7 +207,8 @@ int socp_dense_destroy(socp_dense* h);
 /* The rank-update plugin: SparseSolver with SqrScaling (spsolver.jl:1-130,
  * sqrscalings.jl:8-214), the solver the reference's own tests and MOI run.
  *   socp_sqr_create      replaces SparseSolver(pr) (spsolver.jl:24-57): A, G
- *                        (and sing) copied into the handle once;
+ *                        and sing (the Problem's type parameter; NULL = no
+ *                        problem is sing) copied into the handle once;
  *   socp_sqr_setup_iter  replaces compute_scaling(cones, ::SqrScaling, s, z)
  *                        (sqrscalings.jl:177-185) + setup_iter(::SparseSolver)
  *                        (spsolver.jl:60-84): W^-2 = D + uu' - vv' per SOC cone,
