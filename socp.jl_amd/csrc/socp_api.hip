@@ -918,7 +918,7 @@ static int sqr_launch(socp_sqr* h, const SqrArgs& a, bool setup) {
   socp_ctx* ctx = h->ctx;
   const void* kern = setup ? sqr_setup_kernel_ptr(a.n) : sqr_solve_kernel_ptr(a.n);
   SqrArgs la = a;
-  la.stamps = setup ? g_stamps : nullptr;
+  la.stamps = g_stamps;
   void* kargs[] = {&la};
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
   HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(64), kargs, h->lds, ctx->stream));

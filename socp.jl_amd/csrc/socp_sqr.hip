@@ -197,6 +197,23 @@ __device__ __forceinline__ void sqr_scaling_cone(Ctx& C, int c) {
   if (bad) lds[L.o_flag] = (double)SQR_DOMAIN;
 }
 
+// sum_i p[i * stride] * v[i], i < cnt, in order; the loads are issued U at
+// a time so one memory latency is paid per U elements, not per element
+template <int U = 8>
+__device__ __forceinline__ double dot_strided(const double* p, int64_t stride, const double* v, int cnt) {
+  double acc = 0.0;
+  int i = 0;
+  for (; i + U <= cnt; i += U) {
+    double g[U];
+#pragma unroll
+    for (int t = 0; t < U; ++t) g[t] = p[(int64_t)(i + t) * stride];
+#pragma unroll
+    for (int t = 0; t < U; ++t) acc += g[t] * v[i + t];
+  }
+  for (; i < cnt; ++i) acc += p[(int64_t)i * stride] * v[i];
+  return acc;
+}
+
 // ------------------------------------------------------------ factor ops
 // L y = b (forward): lane i holds row i of L in h[], b[i] in b; returns y.
 template <int NC>
@@ -534,17 +551,15 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
     if (lane == 0) a.status[p] = status;
     return;
   }
-  double h[NC];
-  // rows n..NC-1 as identity rows ([L 0; 0 I]): no guards in the solves
-#pragma unroll
-  for (int j = 0; j < NC; ++j) h[j] = (j < n && lane < n) ? rec[L.r_L + j * n + lane] : (lane == j ? 1.0 : 0.0);
-  const double rd = lane < n ? 1.0 / rec[L.r_L + lane * n + lane] : 1.0;
   double *Sm = lds + L.o_S, *rdgs = lds + L.o_rdgs;
   for (int e = lane; e < m * m; e += 64) {
     const int i = e % m, j = e / m;
     if (i > j) Sm[j * L.ldm + i] = rec[L.r_S + e];
     if (i == j) rdgs[i] = 1.0 / rec[L.r_S + e];
   }
+#ifdef SOCP_DIAG
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
   double *lam = lds + L.o_l, *wb = lds + L.o_wb, *mu = lds + L.o_mu;
   double *dz = lds + L.o_s, *ds = lds + L.o_z;  // the setup's s, z slots
   double *k0 = lds + L.o_D, *k1 = lds + L.o_iW, *k2 = lds + L.o_u, *kt = lds + L.o_v;
@@ -566,25 +581,32 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
     cone_scale(wb, mu[c], k2, k1, o, d, kd, true, lane);
     cone_scale(wb, mu[c], k1, k1, o, d, kd, true, lane);
   }
+  SQ_STAMP(8);
   // n0 = G' k1 + dx (+ A' dy)   (:97-102): a lane per column
   double n0 = 0.0;
   if (lane < n) {
-    for (int i = 0; i < k; ++i) n0 += G[(int64_t)lane * k + i] * k1[i];
+    n0 = dot_strided(G + (int64_t)lane * k, 1, k1, k);
     n0 += a.dx[p * n + lane];
-    if (sing)
-      for (int r = 0; r < m; ++r) n0 += A[(int64_t)lane * m + r] * a.dy[p * m + r];
+    if (sing) n0 += dot_strided(A + (int64_t)lane * m, 1, a.dy + p * m, m);
   }
+  // the factor rows into registers (after the G' mat-vec: not live during it);
+  // rows n..NC-1 as identity rows ([L 0; 0 I]): no guards in the solves
+  double h[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) h[j] = (j < n && lane < n) ? rec[L.r_L + j * n + lane] : (lane == j ? 1.0 : 0.0);
+  const double rd = lane < n ? 1.0 / rec[L.r_L + lane * n + lane] : 1.0;
+  SQ_STAMP(9);
   // n1 = H^-1 n0 (:104-107)
-  const double n1 = bwd_solve<NC>(h, rd, n, fwd_solve<NC>(h, rd, n, n0, lane), lane);
+  const double y0 = fwd_solve<NC>(h, rd, n, n0, lane);
+  SQ_STAMP(10);
+  const double n1 = bwd_solve<NC>(h, rd, n, y0, lane);
+  SQ_STAMP(11);
   if (m > 0) {
     // m0 = A n1 - dy; cy = S^-1 m0; m0 = sing ? dy - cy : -cy   (:108-118)
     if (lane < n) nv[lane] = n1;
     wsync();
     double t = 0.0;
-    if (lane < m) {
-      for (int j = 0; j < n; ++j) t += A[(int64_t)j * m + lane] * nv[j];
-      t -= a.dy[p * m + lane];
-    }
+    if (lane < m) t = dot_strided(A + lane, m, nv, n) - a.dy[p * m + lane];
     const double cy = chol_solve_lds(Sm, L.ldm, rdgs, m, t, lane);
     if (lane < m) {
       a.cy[p * m + lane] = cy;
@@ -593,22 +615,19 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
     }
     wsync();
     // n0 += A' m0   (:119-120)
-    if (lane < n)
-      for (int r = 0; r < m; ++r) n0 += A[(int64_t)lane * m + r] * mv[r];
+    if (lane < n) n0 += dot_strided(A + (int64_t)lane * m, 1, mv, m);
   }
+  SQ_STAMP(12);
   // cx = H^-1 n0 (:122-124)
   const double cx = bwd_solve<NC>(h, rd, n, fwd_solve<NC>(h, rd, n, n0, lane), lane);
+  SQ_STAMP(13);
   if (lane < n) {
     a.cx[p * n + lane] = cx;
     nv[lane] = cx;
   }
   wsync();
   // k1 = G cx - k2 (:125-126), a lane per row
-  for (int i = lane; i < k; i += 64) {
-    double t = 0.0;
-    for (int j = 0; j < n; ++j) t += G[(int64_t)j * k + i] * nv[j];
-    kt[i] = t - k2[i];
-  }
+  for (int i = lane; i < k; i += 64) kt[i] = dot_strided(G + i, k, nv, n) - k2[i];
   // cz = W^-1 W^-1 k1; k1 = W cz; k0 -= k1; cs = W k0   (:127-131)
   double *cz = k2, *cs = k1;
   for (int c = 0; c < nc; ++c) {
@@ -625,6 +644,7 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
     a.cs[p * k + i] = cs[i];
   }
   if (lane == 0) a.status[p] = 0;
+  SQ_STAMP(14);
 }
 
 }  // namespace
@@ -638,7 +658,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void so
 }
 
 template <int NC>
-__global__ __launch_bounds__(64) void socp_sqr_solve_kernel(SqrArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void socp_sqr_solve_kernel(SqrArgs a) {
   extern __shared__ double lds_dyn[];
   const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
   Ctx C{a, L, lds_dyn, (int)threadIdx.x};

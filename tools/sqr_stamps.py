@@ -31,3 +31,14 @@ tot = v[:7].sum()
 print(f"== {cfg.name} B={B} setup kernel {ms:.3f} ms, cycles/problem {tot / B:.0f}")
 for nm, x in zip(names, v[:7]):
     print(f"   {nm:14s} {x / B:9.0f} cyc  {100 * x / tot:5.1f}%")
+buf.zero_()
+r = [torch.randn(B * q, dtype=torch.float64, device="cuda") for q in (cfg.n, cfg.m, cfg.k, cfg.k)]
+hd.solve_kkt(*r)
+ctx.sync()
+ms = ctx.last_kernel_ms()
+v = buf.cpu().numpy().astype(float)
+sn = ["load+cone head", "G'k1", "fwd #1", "bwd #1", "A,S,A'", "fwd+bwd #2", "Gcx+cone tail"]
+tot = v[8:15].sum()
+print(f"== solve kernel {ms:.3f} ms, cycles/problem {tot / B:.0f}")
+for nm, x in zip(sn, v[8:15]):
+    print(f"   {nm:14s} {x / B:9.0f} cyc  {100 * x / tot:5.1f}%")
