@@ -214,6 +214,16 @@ __device__ __forceinline__ double dot_strided(const double* p, int64_t stride, c
   return acc;
 }
 
+// 1/sqrt(x) from v_rsq_f64 refined by two Newton steps (to within an ulp or
+// two; x <= 0 or NaN gives NaN or inf, which the callers' status checks catch)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = y * (1.5 - hx * y * y);
+  y = y * (1.5 - hx * y * y);
+  return y;
+}
+
 // ------------------------------------------------------------ factor ops
 // L y = b (forward): lane i holds row i of L in h[], b[i] in b; returns y.
 template <int NC>
@@ -247,7 +257,7 @@ __device__ __forceinline__ double bwd_solve(const double (&h)[NC], double rd, in
 __device__ __forceinline__ bool mod_step(double& hj, double& w, double& rd, int j, double sig, int lane) {
   const double ljj = bcast(hj, j), wj = bcast(w, j), il = bcast(rd, j);
   const double r2 = ljj * ljj + sig * wj * wj;
-  const double r = sqrt(r2), ir = 1.0 / r;
+  const double ir = rsqrt_nr(r2), r = r2 * ir;
   const double cc = r * il, sn = wj * il, icc = ljj * ir;
   if (lane == j) {
     hj = r;
@@ -415,7 +425,7 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
       if (j >= n) continue;  // one uniform branch per column (the padded pivots are 1)
       const double d = bcast(h[j], j);
       badc |= !(d > 0.0);
-      const double r = sqrt(d), ir = 1.0 / r;
+      const double ir = rsqrt_nr(d), r = d * ir;
       if (lane == j) {
         h[j] = r;
         rd = ir;
