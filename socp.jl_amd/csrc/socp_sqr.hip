@@ -277,7 +277,7 @@ __device__ __forceinline__ bool chol_lds(double* Sm, int ld, int m, double* rdg,
     wsync();
     const double djj = Sm[j * ld + j];
     if (!(djj > 0.0)) return false;
-    const double r = sqrt(djj), ir = 1.0 / r;
+    const double ir = rsqrt_nr(djj), r = djj * ir;
     if (lane == j) {
       Sm[j * ld + j] = r;
       rdg[j] = ir;
