@@ -503,11 +503,7 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
       // one entry (r, q), r >= q, per lane: independent dot products
       for (int e = lane; e < m * m; e += 64) {
         const int r = e % m, q = e / m;
-        if (r >= q) {
-          double s = 0.0;
-          for (int i = 0; i < n; ++i) s += Cm[r * L.ldl + i] * Cm[q * L.ldl + i];
-          Sm[q * L.ldm + r] = s;
-        }
+        if (r >= q) Sm[q * L.ldm + r] = dot_strided(Cm + r * L.ldl, 1, Cm + q * L.ldl, n);
       }
       if (!chol_lds(Sm, L.ldm, m, lds + L.o_rdgs, lane)) status = SQR_CHOL_S;
       SQ_STAMP(5);
