@@ -374,46 +374,25 @@ def main():
     c, A, b, G, h = S.generate(cfg.cones, B, n, m, k, cfg.seed, first_problem=rank * B, ctx=ctx)
     sing = torch.zeros(B, dtype=torch.uint8, device=dev)  # uniform G (k > n) has full column rank
     ctx.sync()
-    out = None
-    gathered = None
-    if world > 1:
-        from socp_amd.dist import gather_outcomes
-
-    def step():
-        nonlocal out, gathered
-        out = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=tol, ctx=ctx, out=out,
-                            res=world > 1)
-        if world > 1:
-            # the path's only exchange: every problem's 32-byte outcome record
-            # (status, iters, ||rd||, ||rp||, z's) to every rank, on torch's stream
-            gathered = gather_outcomes(out["status"], out["iters"], out["res"])
-
-    for _ in range(args.warmup):
-        step()
-    ctx.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    from socp_amd.dist import timed_shard_steps
     kernel_ms = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    prev = {"out": None}
+
+    def solve_shard():
+        prev["out"] = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=tol, ctx=ctx,
+                                    out=prev["out"], res=world > 1)
         kernel_ms.append(ctx.last_kernel_ms())  # HIP events around the solver launch
-    ctx.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    iters_local = int(out["iters"].sum().item()) * args.steps
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-        it = torch.tensor([iters_local], dtype=torch.int64, device=dev)
-        dist.all_reduce(it)
-        iters_total = int(it.item())
-    else:
-        iters_total = iters_local
+        return prev["out"]
+
+    def sync():
+        ctx.sync()
+        torch.cuda.synchronize()
+
+    # warm-up, the K timed steps between barriers, max-over-ranks time, summed
+    # iterations, and (N > 1) the per-step outcome all-gather: socp_amd.dist
+    tr = timed_shard_steps(solve_shard, args.steps, args.warmup, sync=sync)
+    kernel_ms = kernel_ms[args.warmup:]
+    out, dt, iters_total = tr["out"], tr["dt"], tr["iters_total"]
     status_counts = torch.bincount(out["status"].long(), minlength=5).tolist()
 
     if rank == 0:

@@ -60,7 +60,8 @@ struct socp_ctx {
   int device = 0;
   hipStream_t own = nullptr;     // created by socp_ctx_create
   hipStream_t stream = nullptr;  // where work goes: `own`, or the caller's (socp_ctx_set_stream)
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // timing pair (socp_last_kernel_ms)
+  hipEvent_t evh = nullptr;                 // stream hand-off (ctx_switch_stream), never a timing event
   int num_cu = 0;
   float last_ms = 0.f;
   const char* last_name = "";
@@ -89,11 +90,14 @@ extern "C" void socp_params_default(socp_params* p) {
 static void ctx_free(socp_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  // NULL is the null stream (socp_ctx_set_stream(NULL)): synchronise it too,
+  // so no kernel still reads the buffers released below
+  (void)hipStreamSynchronize(c->stream);
   if (c->own && c->own != c->stream) (void)hipStreamSynchronize(c->own);
   for (auto& b : c->buf) b.release();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->evh) (void)hipEventDestroy(c->evh);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
@@ -121,6 +125,7 @@ extern "C" int socp_ctx_create(int device, socp_ctx** out) {
   c->stream = c->own;
   if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail(e, "hipEventCreate");
   if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail(e, "hipEventCreate");
+  if ((e = hipEventCreateWithFlags(&c->evh, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
   *out = c;
   return 0;
 }
@@ -134,8 +139,8 @@ static int ctx_switch_stream(socp_ctx* c, hipStream_t s) {
   if (s == c->stream) return 0;
   // work already queued on the old stream stays ordered before what follows
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipEventRecord(c->ev1, c->stream));
-  HIPCHK(hipStreamWaitEvent(s, c->ev1, 0));
+  HIPCHK(hipEventRecord(c->evh, c->stream));
+  HIPCHK(hipStreamWaitEvent(s, c->evh, 0));
   c->stream = s;
   return 0;
 }
@@ -702,6 +707,8 @@ extern "C" int socp_dense_create(socp_ctx* ctx, const socp_dims* dims, const int
   a.counter = (int32_t*)h->buf[D::D_CNT].p;
   a.rec = (double*)h->buf[D::D_REC].p;
   a.rec_stride = h->rec_stride;
+  // host sources may be pageable temporaries the caller frees on return
+  if (!dev && hipStreamSynchronize(ctx->stream) != hipSuccess) return bail(fail(SOCP_E_HIP, "hipStreamSynchronize"));
   *out = h;
   return 0;
 }
@@ -905,6 +912,9 @@ extern "C" int socp_sqr_create(socp_ctx* ctx, const socp_dims* dims, const int32
     if (h->lds > 64 * 1024 &&
         hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds) != hipSuccess)
       return bail(fail(SOCP_E_HIP, "hipFuncSetAttribute"));
+  // host sources may be pageable temporaries the caller frees on return
+  if (!h->dev && hipStreamSynchronize(ctx->stream) != hipSuccess)
+    return bail(fail(SOCP_E_HIP, "hipStreamSynchronize"));
   *out = h;
   return 0;
 }
@@ -1272,7 +1282,8 @@ inline size_t al_up(size_t v) { return (v + kAl - 1) / kAl * kAl; }
 struct IngestSlot {
   void* pin_in = nullptr;
   void* pin_out = nullptr;
-  size_t pin_in_cap = 0, pin_out_cap = 0;
+  void* pin_csc = nullptr;  // CSC staging, grown on its own so pin_in never moves
+  size_t pin_in_cap = 0, pin_out_cap = 0, pin_csc_cap = 0;
   DevBuf dev_in, dev_out, dev_csc;
   hipEvent_t ready = nullptr, solved = nullptr, done = nullptr;
   int64_t ticket = -1;  // outstanding ticket, -1 when free
@@ -1358,6 +1369,7 @@ static void ingest_free(socp_ingest* g) {
   for (auto& sl : g->slot) {
     if (sl.pin_in) (void)hipHostFree(sl.pin_in);
     if (sl.pin_out) (void)hipHostFree(sl.pin_out);
+    if (sl.pin_csc) (void)hipHostFree(sl.pin_csc);
     sl.dev_in.release();
     sl.dev_out.release();
     sl.dev_csc.release();
@@ -1565,9 +1577,9 @@ extern "C" int socp_ingest_submit_csc(socp_ingest* g, int64_t batch, const doubl
   for (int i = 0; i < 4; ++i) par_copy(pin + off[i], src[i], nb[i]);
   for (int i = 0; i < 4; ++i)
     if (src[i] && nb[i]) HIPCHK(hipMemcpyAsync(din + off[i], pin + off[i], nb[i], hipMemcpyHostToDevice, g->h2d));
-  // the CSC arrays: sizes from the host offsets; staged through the slot's
-  // pinned output block's tail would race with results, so they get pinned
-  // space of their own after the dense inputs (grown on demand)
+  // the CSC arrays: sizes from the host offsets; staged in the slot's own
+  // pinned CSC block (grown on demand), so the pinned input block -- and the
+  // pointers socp_ingest_next_inputs handed out for it -- never move
   const int64_t nzA = (d.m > 0 && B > 0) ? A_nz_offs[B] - A_nz_offs[0] : 0;
   const int64_t nzG = B > 0 ? G_nz_offs[B] - G_nz_offs[0] : 0;
   if (nzA < 0 || nzG < 0) return fail(SOCP_E_INVALID, "nz_offs must be non-decreasing");
@@ -1582,22 +1594,21 @@ extern "C" int socp_ingest_submit_csc(socp_ingest* g, int64_t batch, const doubl
   const size_t oGr = o;  o += al_up(sizeof(int64_t) * (nzG + 1));
   const size_t oGv = o;  o += al_up(sizeof(double) * (nzG + 1));
   const size_t csc_bytes = o;
-  // pinned CSC staging: the input block is regrown (its dense part re-copied)
-  if (L.total + csc_bytes > sl.pin_in_cap) {
-    void* np = nullptr;
-    if (hipHostMalloc(&np, L.total + csc_bytes, hipHostMallocDefault) != hipSuccess)
+  if (csc_bytes > sl.pin_csc_cap) {
+    // the slot is free (ingest_begin); drain the copy stream anyway before
+    // the old block goes
+    HIPCHK(hipStreamSynchronize(g->h2d));
+    if (sl.pin_csc) (void)hipHostFree(sl.pin_csc);
+    sl.pin_csc = nullptr;
+    sl.pin_csc_cap = 0;
+    if (hipHostMalloc(&sl.pin_csc, csc_bytes, hipHostMallocDefault) != hipSuccess)
       return fail(SOCP_E_NOMEM, "pinned host allocation failed");
-    HIPCHK(hipStreamSynchronize(g->h2d));  // the dense copies above read the old block
-    memcpy(np, sl.pin_in, L.total);
-    (void)hipHostFree(sl.pin_in);
-    sl.pin_in = np;
-    sl.pin_in_cap = L.total + csc_bytes;
-    pin = (char*)sl.pin_in;
+    sl.pin_csc_cap = csc_bytes;
   }
   // device: the CSC arrays, then the dense A and G they are packed into
   const size_t dA = al_up(sizeof(double) * B * d.m * d.n), dG = al_up(sizeof(double) * B * d.k * d.n);
   if (sl.dev_csc.ensure(csc_bytes + dA + dG)) return fail(SOCP_E_NOMEM, "device allocation failed");
-  char* pc = pin + L.total;
+  char* pc = (char*)sl.pin_csc;
   char* dc = (char*)sl.dev_csc.p;
   // offsets are rebased to start at 0 for the pack kernel
   auto put_offs = [&](size_t off_, const int64_t* v) {

@@ -280,8 +280,9 @@ end
 
 # ------------------------------------------------------- multi-GPU gather
 # One process per GPU (e.g. under MPI.jl); problems shard by contiguous global
-# index and the only collective is the RCCL all-gather of (status, iters)
-# (include/socp.h: socp_comm_*, socp_allgather_status).  Rank 0 makes the id,
+# index and the only collective is the RCCL all-gather of each problem's
+# 32-byte outcome record (include/socp.h: socp_comm_*, socp_allgather_outcomes;
+# socp_allgather_status gathers only (status, iters)).  Rank 0 makes the id,
 # the host broadcasts it (MPI.Bcast! below is the usual way).
 const SOCP_COMM_ID_BYTES = 128
 
@@ -306,6 +307,29 @@ function socp_allgather_status(comm::Ptr{Cvoid}, B::Integer, status::Ptr{Int32},
                                out::Ptr{Int32})
     socp_check(ccall((:socp_allgather_status, libsocp), Cint,
                      (Ptr{Cvoid}, Int64, Ptr{Int32}, Ptr{Int32}, Ptr{Int32}), comm, B, status, iters, out))
+    socp_check(ccall((:socp_ctx_sync, libsocp), Cint, (Ptr{Cvoid},), socp_ctx()))
+    return nothing
+end
+
+# The 32-byte per-problem outcome record of include/socp.h (socp_outcome): the
+# exit-test quantities of solver.jl:109-122 at the returned iterate.
+struct SocpOutcome
+    status::Int32
+    iters::Int32
+    res_dual::Float64    # ||A'y + G'z + c||
+    res_primal::Float64  # ||Ax - b||
+    gap::Float64         # z's
+end
+
+# status, iters (B Int32 each), res (3B Float64: ||rd||, ||rp||, z's per problem,
+# as socp_batch_solve_ex writes them; C_NULL gives NaN residuals) and out
+# (nranks * B SocpOutcome, rank-major: out[r*B + p] is rank r's problem p) are
+# device pointers; returns after the gather has completed.
+function socp_allgather_outcomes(comm::Ptr{Cvoid}, B::Integer, status::Ptr{Int32}, iters::Ptr{Int32},
+                                 res::Ptr{Float64}, out::Ptr{SocpOutcome})
+    socp_check(ccall((:socp_allgather_outcomes, libsocp), Cint,
+                     (Ptr{Cvoid}, Int64, Ptr{Int32}, Ptr{Int32}, Ptr{Float64}, Ptr{SocpOutcome}),
+                     comm, B, status, iters, res, out))
     socp_check(ccall((:socp_ctx_sync, libsocp), Cint, (Ptr{Cvoid},), socp_ctx()))
     return nothing
 end

@@ -22,13 +22,16 @@ def pack_outcomes(status, iters, res=None):
     z's (socp_outcome layout; NaN residuals when `res` is None)."""
     import torch
     B = status.numel()
-    rec = torch.empty((B, 4), dtype=torch.float64, device=status.device)
-    pair = torch.stack([status.to(torch.int32).reshape(-1), iters.to(torch.int32).reshape(-1)], dim=1)
-    rec[:, 0] = pair.contiguous().view(torch.float64).reshape(-1)
+    # int32 [B, 8]: slots 0-1 the integers, slots 2-7 the three doubles' bit
+    # patterns (int32 views), so no integer bits pass through a floating-point copy
+    rec = torch.empty((B, 8), dtype=torch.int32, device=status.device)
+    rec[:, 0] = status.reshape(-1).to(torch.int32)
+    rec[:, 1] = iters.reshape(-1).to(torch.int32)
     if res is None:
-        rec[:, 1:] = float("nan")
+        r = torch.full((B, 3), float("nan"), dtype=torch.float64, device=status.device)
     else:
-        rec[:, 1:] = res.reshape(B, 3).to(torch.float64)
+        r = res.reshape(B, 3).to(torch.float64).contiguous()
+    rec[:, 2:] = r.view(torch.int32).reshape(B, 6)
     return rec.view(torch.uint8)
 
 
@@ -36,9 +39,9 @@ def unpack_outcomes(rec):
     """[..., 32] uint8 records -> dict(status, iters: int32 [...], res: float64 [..., 3])."""
     import torch
     lead = rec.shape[:-1]
-    f = rec.contiguous().view(torch.float64).reshape(*lead, 4)
-    pair = f[..., 0].contiguous().view(torch.int32).reshape(*lead, 2)
-    return {"status": pair[..., 0], "iters": pair[..., 1], "res": f[..., 1:]}
+    w = rec.contiguous().view(torch.int32).reshape(*lead, 8)
+    res = w[..., 2:].contiguous().view(torch.float64).reshape(*lead, 3)
+    return {"status": w[..., 0].contiguous(), "iters": w[..., 1].contiguous(), "res": res}
 
 
 def gather_outcomes(status, iters, res=None, group=None):
@@ -88,6 +91,7 @@ class StatusComm:
         import torch
         from . import _lib
         B = status.numel()
+        self.ctx.bind_torch_stream()  # the conversions below run on torch's stream
         out = torch.empty((self.nranks, B, 2), dtype=torch.int32, device=status.device)
         st = status.to(torch.int32).contiguous()
         it = iters.to(torch.int32).contiguous()
@@ -101,6 +105,7 @@ class StatusComm:
         import torch
         from . import _lib
         B = status.numel()
+        self.ctx.bind_torch_stream()  # the conversions below run on torch's stream
         out = torch.empty((self.nranks, B, RECORD_BYTES), dtype=torch.uint8, device=status.device)
         st = status.to(torch.int32).contiguous()
         it = iters.to(torch.int32).contiguous()
@@ -114,3 +119,59 @@ class StatusComm:
         if self.handle:
             self._L.socp_comm_destroy(self.handle)
             self.handle = None
+
+
+def timed_shard_steps(solve_shard, steps: int, warmup: int, sync=None):
+    """bench.py's per-rank step loop and accounting (driver contract), for any
+    process-group backend (nccl = RCCL on the GPU box, gloo on the CPU).
+
+    solve_shard() -> dict(status, iters, res) solves this rank's shard once; a
+    step is that solve plus (world > 1) the all-gather of every problem's
+    32-byte outcome record -- the path's only exchange.  W untimed warm-up
+    steps, then exactly `steps` steps bracketed by sync() + barrier on both
+    sides; the elapsed time is the MAX over ranks and the iteration count the
+    SUM over ranks of the problem-iterations each rank executed.
+
+    Returns dict(dt, iters_total, iters_local, out (the last local result),
+    gathered (the last gathered records, world > 1), step_ms (per-step wall
+    time on this rank))."""
+    import time
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    sync = sync or (lambda: None)
+    st = {"out": None, "gathered": None}
+
+    def step():
+        st["out"] = solve_shard()
+        if world > 1:
+            o = st["out"]
+            st["gathered"] = gather_outcomes(o["status"], o["iters"], o.get("res"))
+
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    step_ms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        t1 = time.perf_counter()
+        step()
+        step_ms.append((time.perf_counter() - t1) * 1e3)
+    sync()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    iters_local = int(st["out"]["iters"].sum().item()) * steps
+    iters_total = iters_local
+    if world > 1:
+        dev = st["out"]["iters"].device
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        it = torch.tensor([iters_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(it)
+        iters_total = int(it.item())
+    return {"dt": dt, "iters_total": iters_total, "iters_local": iters_local, "out": st["out"],
+            "gathered": st["gathered"], "step_ms": step_ms}

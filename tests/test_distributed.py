@@ -139,3 +139,101 @@ def test_abi_status_gather_single_rank():
         assert (rec["res"][0][conv].sum(dim=1) < 1e-5).all()
     finally:
         comm.close()
+
+
+def _bench_worker(rank, world, port, total, steps, q):
+    """One rank of bench.py's N>1 loop (socp_amd.dist.timed_shard_steps) over
+    gloo, with the oracle as the per-rank shard solve."""
+    import sys
+    import time
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path.insert(0, os.path.join(root, "socp.jl_amd"))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from socp_amd.configs import C1
+    from socp_amd.dist import shard_range, timed_shard_steps
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_range(total, rank, world)
+    cfg = C1
+    d = O.generate(cfg.cones, hi - lo, cfg.n, cfg.m, cfg.k, cfg.seed, first_problem=lo)
+    calls = []
+
+    def solve_shard():
+        if rank == 1:
+            time.sleep(0.05)  # a slower rank: the reported time must be the max
+        r = O.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                          params=O.Params(maxit=40, tol=1e-5), nthreads=1)
+        calls.append(1)
+        return {key: torch.from_numpy(r[key]) for key in ("status", "iters", "res")}
+
+    tr = timed_shard_steps(solve_shard, steps, 1)
+    q.put({"rank": rank, "dt": tr["dt"], "iters_total": tr["iters_total"], "iters_local": tr["iters_local"],
+           "calls": len(calls), "step_ms": tr["step_ms"],
+           "gathered": {key: v.numpy() for key, v in tr["gathered"].items()}})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_step_accounting_gloo_world2(oracle):
+    """bench.py's N>1 accounting on the CPU: two gloo ranks run the timed step
+    loop; the iteration total, the max-over-ranks time and the gathered
+    records equal what a single process computes for the whole batch."""
+    from socp_amd.configs import C1
+    total, world, steps = 8, 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, total, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=180) for _ in range(world)], key=lambda g: g["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cfg = C1
+    d = oracle.generate(cfg.cones, total, cfg.n, cfg.m, cfg.k, cfg.seed)
+    r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                           params=oracle.Params(maxit=40, tol=1e-5), nthreads=1)
+    single_iters = int(r["iters"].sum()) * steps
+    for g in got:
+        assert g["calls"] == steps + 1  # one warm-up step, then exactly `steps`
+        assert g["iters_total"] == single_iters
+        assert np.array_equal(g["gathered"]["status"].reshape(-1), r["status"])
+        assert np.array_equal(g["gathered"]["iters"].reshape(-1), r["iters"])
+        assert np.array_equal(g["gathered"]["res"].reshape(total, 3), r["res"])
+    assert got[0]["iters_local"] + got[1]["iters_local"] == single_iters
+    # every rank reports the same, max-over-ranks time, at least the slow rank's own steps
+    assert got[0]["dt"] == got[1]["dt"]
+    assert got[0]["dt"] >= sum(got[1]["step_ms"]) / 1e3 - 1e-6
+    assert got[0]["dt"] >= steps * 0.05
+
+
+@pytest.mark.gpu
+def test_abi_outcome_gather_fresh_context_converted_inputs():
+    """socp_allgather_outcomes on a fresh Context whose stream nothing has bound
+    yet, with int64 status / iters and float32 residuals: the conversions run
+    on torch's stream and the gather must see them (StatusComm binds the
+    context to torch's stream first)."""
+    import torch
+    import socp_amd as S
+    from socp_amd.dist import StatusComm
+    ctx = S.Context(0)
+    comm = StatusComm(ctx, 1, 0, StatusComm.unique_id())
+    try:
+        for B in (1, 4097, 200000):
+            st = torch.randint(0, 5, (B,), dtype=torch.int64, device="cuda")
+            it = torch.randint(0, 41, (B,), dtype=torch.int64, device="cuda")
+            res = torch.rand((B, 3), dtype=torch.float32, device="cuda") * 1e-3
+            rec = comm.allgather_outcomes(st, it, res)
+            assert torch.equal(rec["status"][0], st.to(torch.int32))
+            assert torch.equal(rec["iters"][0], it.to(torch.int32))
+            assert torch.equal(rec["res"][0], res.to(torch.float64))
+            out = comm.allgather_status(st, it)
+            assert torch.equal(out[0, :, 0], st.to(torch.int32)) and torch.equal(out[0, :, 1], it.to(torch.int32))
+    finally:
+        comm.close()
