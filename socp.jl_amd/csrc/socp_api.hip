@@ -824,7 +824,7 @@ static void sqr_free(socp_sqr* h) {
 }
 
 static bool sqr_fits(const socp_dims* d, size_t* lds) {
-  if (d->n > SQR_NMAX || d->m > SQR_NMAX || d->k > SQR_KMAX) return false;
+  if (d->n > SQR_LMAX || d->m > SQR_LMAX || d->k > SQR_KMAX) return false;
   const size_t bytes = (size_t)sqr_layout(d->n, d->m, d->k, d->ncones).total * sizeof(double);
   if (lds) *lds = bytes;
   return bytes <= 160 * 1024;
@@ -873,7 +873,7 @@ extern "C" int socp_sqr_create(socp_ctx* ctx, const socp_dims* dims, const int32
   int rc = check_problem(dims, cone_kind, cone_offs, cone_dim, &a.cones, &degree);
   if (rc) return bail(rc);
   if (!sqr_fits(dims, &h->lds))
-    return bail(fail(SOCP_E_UNSUPPORTED, "rank-update plugin: n, m <= 64, k <= 256 (socp_sqr.hip)"));
+    return bail(fail(SOCP_E_UNSUPPORTED, "rank-update plugin: n, m <= 160, k <= 256, LDS layout <= 160 KiB (socp_sqr.hip)"));
   const int64_t B = dims->batch;
   const int n = dims->n, m = dims->m, k = dims->k;
   if (B > 0 && (!G || (m > 0 && !A))) return bail(fail(SOCP_E_INVALID, "NULL data pointer"));
@@ -907,7 +907,7 @@ extern "C" int socp_sqr_create(socp_ctx* ctx, const socp_dims* dims, const int32
   if (h->buf[Q::Q_REC].ensure((size_t)B * (size_t)h->L.rec * sizeof(double)))
     return bail(fail(SOCP_E_NOMEM, "factor record allocation failed"));
   a.rec = (double*)h->buf[Q::Q_REC].p;
-  const void* kerns[2] = {sqr_setup_kernel_ptr(n), sqr_solve_kernel_ptr(n)};
+  const void* kerns[2] = {sqr_setup_kernel_ptr(n, m), sqr_solve_kernel_ptr(n, m)};
   for (const void* kern : kerns)
     if (h->lds > 64 * 1024 &&
         hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds) != hipSuccess)
@@ -926,14 +926,16 @@ extern "C" int socp_sqr_destroy(socp_sqr* h) {
 
 static int sqr_launch(socp_sqr* h, const SqrArgs& a, bool setup) {
   socp_ctx* ctx = h->ctx;
-  const void* kern = setup ? sqr_setup_kernel_ptr(a.n) : sqr_solve_kernel_ptr(a.n);
+  const void* kern = setup ? sqr_setup_kernel_ptr(a.n, a.m) : sqr_solve_kernel_ptr(a.n, a.m);
   SqrArgs la = a;
   la.stamps = g_stamps;
   void* kargs[] = {&la};
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
-  HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(64), kargs, h->lds, ctx->stream));
+  const int nt = sqr_block_threads(a.n, a.m);
+  HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(nt), kargs, h->lds, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
-  ctx->last_name = setup ? "socp_sqr_setup_kernel" : "socp_sqr_solve_kernel";
+  ctx->last_name = nt > 64 ? (setup ? "socp_sqr_setup_wg_kernel" : "socp_sqr_solve_wg_kernel")
+                           : (setup ? "socp_sqr_setup_kernel" : "socp_sqr_solve_kernel");
   return 0;
 }
 

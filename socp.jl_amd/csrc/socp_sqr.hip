@@ -653,6 +653,377 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
   SQ_STAMP(14);
 }
 
+
+// ================================================ workgroup kernels (n, m <= 160)
+// One SQR_LT-thread workgroup (4 wavefronts) per problem for shapes whose
+// factor does not fit one wavefront's registers -- the reference's own
+// optimal-control problem (runtests.jl:204-244, n = 150, m = 102) among them.
+// The factor lives packed (lower triangle, column-major) in LDS; C = L^-1 A'
+// is formed 16 right-hand sides at a time and kept in the record's scratch;
+// H and S = C'C are lower 16 x 16 tiles of f64 MFMA 16x16x4 dealt out to the
+// four wavefronts.  The cone operations run on wavefront 0 (the wavefront
+// helpers above); the column recurrences take one barrier per column.
+
+__device__ __forceinline__ void bar() { __syncthreads(); }
+
+// lower 16x16 tiles of X'Y (+ X2'X2) into the packed LDS triangle P (N x N):
+// X[r][a] = fa[r] * src[a * ld + r], Y[r][b] = fb[r] * src[b * ld + r] for
+// r < rows (fa / fb NULL: 1); with src2, the unscaled rows of src2 (rows2 x N,
+// leading dimension ld2) are added to the same accumulators.
+__device__ __forceinline__ void syrk_tiles(const double* src, int ld, int rows, const double* fa, const double* fb,
+                                           const double* src2, int ld2, int rows2, int N, double* P, int tid) {
+  typedef double d4v __attribute__((ext_vector_type(4)));
+  const int w = tid >> 6, lane = tid & 63, cl = lane & 15, kk = lane >> 4;
+  const int NT = (N + 15) / 16;
+  for (int t = w; t < NT * (NT + 1) / 2; t += SQR_LT / 64) {
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    const int a = 16 * I + cl, b = 16 * J + cl;
+    const bool va = a < N, vb = b < N;
+    d4v acc = {0.0, 0.0, 0.0, 0.0};
+    for (int r0 = 0; r0 < rows; r0 += 4) {
+      const int r = r0 + kk;
+      const bool vr = r < rows;
+      double xa = (vr && va) ? src[(int64_t)a * ld + r] : 0.0;
+      double yb = (vr && vb) ? src[(int64_t)b * ld + r] : 0.0;
+      if (fa && vr) xa *= fa[r];
+      if (fb && vr) yb *= fb[r];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, yb, acc, 0, 0, 0);
+    }
+    if (src2)
+      for (int r0 = 0; r0 < rows2; r0 += 4) {
+        const int r = r0 + kk;
+        const bool vr = r < rows2;
+        const double xa = (vr && va) ? src2[(int64_t)a * ld2 + r] : 0.0;
+        const double yb = (vr && vb) ? src2[(int64_t)b * ld2 + r] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, yb, acc, 0, 0, 0);
+      }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int row = 16 * I + kk + 4 * v, col = 16 * J + cl;
+      if (row < N && col <= row) P[sqr_pk(row, col, N)] = acc[v];
+    }
+  }
+}
+
+// right-looking Cholesky of the packed N x N triangle; 1/diag -> rdg; false at
+// a pivot <= 0 or NaN (the same value in every thread: a uniform exit)
+__device__ __forceinline__ bool chol_packed(double* P, int N, double* rdg, int tid) {
+  for (int j = 0; j < N; ++j) {
+    bar();
+    const double d = P[sqr_pk(j, j, N)];
+    if (!(d > 0.0)) return false;
+    const double ir = rsqrt_nr(d);
+    bar();
+    for (int i = j + tid; i < N; i += SQR_LT) {
+      if (i == j) {
+        P[sqr_pk(j, j, N)] = d * ir;
+        rdg[j] = ir;
+      } else {
+        P[sqr_pk(i, j, N)] *= ir;
+      }
+    }
+    bar();
+    // trailing update L(i, l) -= L(i, j) L(l, j), j < l <= i: 16 x 16 thread grid
+    const int ti = tid >> 4, tl = tid & 15;
+    for (int l = j + 1 + tl; l < N; l += 16) {
+      const double llj = P[sqr_pk(l, j, N)];
+      for (int i = l + ti; i < N; i += 16) P[sqr_pk(i, l, N)] -= P[sqr_pk(i, j, N)] * llj;
+    }
+  }
+  bar();
+  return true;
+}
+
+// L y = b then L' x = y against the packed factor, b in LDS (N), in place
+__device__ __forceinline__ void chol_solve_packed(const double* P, int N, const double* rdg, double* b, int tid) {
+  for (int j = 0; j < N; ++j) {
+    bar();
+    const double xj = b[j] * rdg[j];
+    bar();
+    if (tid == 0) b[j] = xj;
+    for (int i = j + 1 + tid; i < N; i += SQR_LT) b[i] -= P[sqr_pk(i, j, N)] * xj;
+  }
+  for (int j = N - 1; j >= 0; --j) {
+    bar();
+    const double xj = b[j] * rdg[j];
+    bar();
+    if (tid == 0) b[j] = xj;
+    for (int i = tid; i < j; i += SQR_LT) b[i] -= P[sqr_pk(j, i, N)] * xj;
+  }
+  bar();
+}
+
+// the same two triangular solves against a column-major factor in global memory
+// (the record's L_S: m x m, zeros above the diagonal)
+__device__ __forceinline__ void chol_solve_global(const double* F, int N, double* b, int tid) {
+  for (int j = 0; j < N; ++j) {
+    bar();
+    const double xj = b[j] / F[(int64_t)j * N + j];
+    bar();
+    if (tid == 0) b[j] = xj;
+    for (int i = j + 1 + tid; i < N; i += SQR_LT) b[i] -= F[(int64_t)j * N + i] * xj;
+  }
+  for (int j = N - 1; j >= 0; --j) {
+    bar();
+    const double xj = b[j] / F[(int64_t)j * N + j];
+    bar();
+    if (tid == 0) b[j] = xj;
+    for (int i = tid; i < j; i += SQR_LT) b[i] -= F[(int64_t)i * N + j] * xj;
+  }
+  bar();
+}
+
+__device__ __forceinline__ void setup_problem_wg(Ctx& C, int64_t p, int tid) {
+  const SqrArgs& a = C.a;
+  const SqrLayout& L = C.L;
+  double* lds = C.lds;
+  const int n = a.n, m = a.m, k = a.k, nc = a.nc;
+  const double* G = a.G + p * (int64_t)k * n;
+  const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
+  const bool sing = a.sing && a.sing[p];
+  double* rec = a.rec + p * L.rec;
+  double* P = lds + L.o_L;
+  double* rdg = lds + L.o_nv;  // 1 / diag of the current factor
+  for (int i = tid; i < k; i += SQR_LT) {
+    lds[L.o_s + i] = a.s[p * k + i];
+    lds[L.o_z + i] = a.z[p * k + i];
+    lds[L.o_one + i] = 1.0;
+  }
+  if (tid == 0) lds[L.o_flag] = 0.0;
+  bar();
+  if (tid < 64)
+    for (int c = 0; c < nc; ++c) sqr_scaling_cone(C, c);
+  bar();
+  int status = (int)lds[L.o_flag];
+  if (status == 0) {
+    // H = (iW G)'(iW G) (spsolver.jl:62-64), or G'(iWiW G) + A'A when sing (:67-71)
+    if (!sing)
+      syrk_tiles(G, k, k, lds + L.o_iW, lds + L.o_iW, nullptr, 0, 0, n, P, tid);
+    else
+      syrk_tiles(G, k, k, nullptr, lds + L.o_D, m ? A : nullptr, m, m, n, P, tid);
+    if (!chol_packed(P, n, rdg, tid)) status = SQR_CHOL_H;
+  }
+  // modify_factors! (sqrscalings.jl:160-194): per SOC cone the update with
+  // G'u and the downdate with G'v, the downdate chain one column behind
+  for (int c = 0; c < nc && status == 0; ++c) {
+    if (a.cones.kind[c] != SOC_K) continue;
+    const int o = a.cones.offs[c], d = a.cones.dim[c];
+    double *wu = lds + L.o_w, *wv = lds + L.o_wv;
+    bar();
+    for (int col = tid; col < n; col += SQR_LT) {
+      double su = 0.0, sv = 0.0;
+      for (int r = o; r < o + d; ++r) {
+        const double g = G[(int64_t)col * k + r];
+        su += g * lds[L.o_u + r];
+        sv += g * lds[L.o_v + r];
+      }
+      wu[col] = su;
+      wv[col] = sv;
+    }
+    bool bad = false;
+    for (int t = 0; t <= n; ++t) {
+      bar();
+      // chain u at column t, chain v at column t - 1 (its column t - 1 is final for u)
+      const int ju = t, jv = t - 1;
+      double cu = 0, su_ = 0, iu = 0, cv = 0, sv_ = 0, iv = 0, ru = 0, rv = 0;
+      if (ju < n) {
+        const double ljj = P[sqr_pk(ju, ju, n)], wj = wu[ju];
+        const double r2 = ljj * ljj + wj * wj;
+        bad |= !(r2 > 0.0);
+        const double ir = rsqrt_nr(r2);
+        ru = r2 * ir;
+        const double il = 1.0 / ljj;
+        cu = ru * il;
+        su_ = wj * il;
+        iu = ljj * ir;
+      }
+      if (jv >= 0) {
+        const double ljj = P[sqr_pk(jv, jv, n)], wj = wv[jv];
+        const double r2 = ljj * ljj - wj * wj;
+        bad |= !(r2 > 0.0);
+        const double ir = rsqrt_nr(r2);
+        rv = r2 * ir;
+        const double il = 1.0 / ljj;
+        cv = rv * il;
+        sv_ = wj * il;
+        iv = ljj * ir;
+      }
+      bar();
+      if (ju < n) {
+        for (int i = ju + 1 + tid; i < n; i += SQR_LT) {
+          const double lij = (P[sqr_pk(i, ju, n)] + su_ * wu[i]) * iu;
+          P[sqr_pk(i, ju, n)] = lij;
+          wu[i] = cu * wu[i] - su_ * lij;
+        }
+        if (tid == 0) P[sqr_pk(ju, ju, n)] = ru;
+      }
+      if (jv >= 0) {
+        for (int i = jv + 1 + tid; i < n; i += SQR_LT) {
+          const double lij = (P[sqr_pk(i, jv, n)] - sv_ * wv[i]) * iv;
+          P[sqr_pk(i, jv, n)] = lij;
+          wv[i] = cv * wv[i] - sv_ * lij;
+        }
+        if (tid == 0) P[sqr_pk(jv, jv, n)] = rv;
+      }
+    }
+    if (bad) status = SQR_CHOL_H;  // uniform: every thread evaluated the same pivots
+  }
+  bar();
+  if (status == 0) {
+    for (int j = tid; j < n; j += SQR_LT) rdg[j] = 1.0 / P[sqr_pk(j, j, n)];
+    // the factor into the record (column-major, zeros above the diagonal)
+    for (int e = tid; e < n * n; e += SQR_LT) {
+      const int i = e % n, j = e / n;
+      rec[L.r_L + e] = i >= j ? P[sqr_pk(i, j, n)] : 0.0;
+    }
+    bar();
+    if (m > 0) {
+      // C = L^-1 A' (spsolver.jl:80-82), SQR_RC right-hand sides at a time
+      double* Cc = lds + L.o_C;  // Cc[t * n + i]
+      double* Cg = rec + L.r_C;   // C[q * n + i]
+      for (int q0 = 0; q0 < m; q0 += SQR_RC) {
+        const int nr = (m - q0) < SQR_RC ? (m - q0) : SQR_RC;
+        bar();
+        for (int e = tid; e < nr * n; e += SQR_LT) {
+          const int t = e / n, i = e % n;
+          Cc[t * n + i] = A[(int64_t)i * m + q0 + t];
+        }
+        for (int j = 0; j < n; ++j) {
+          bar();
+          const int t = tid & 15;
+          const double xj = t < nr ? Cc[t * n + j] * rdg[j] : 0.0;
+          bar();
+          if (t < nr) {
+            if ((tid >> 4) == 0) Cc[t * n + j] = xj;
+            for (int i = j + 1 + (tid >> 4); i < n; i += SQR_LT / 16) Cc[t * n + i] -= P[sqr_pk(i, j, n)] * xj;
+          }
+        }
+        bar();
+        for (int e = tid; e < nr * n; e += SQR_LT) Cg[(int64_t)q0 * n + e] = Cc[e];
+      }
+      __threadfence_block();
+      bar();
+      // S = C'C (:83) into the packed triangle (L_H is in the record now), chol(S)
+      syrk_tiles(Cg, n, n, nullptr, nullptr, nullptr, 0, 0, m, P, tid);
+      double* rds = lds + L.o_rdgs;
+      if (!chol_packed(P, m, rds, tid)) status = SQR_CHOL_S;
+      if (status == 0)
+        for (int e = tid; e < m * m; e += SQR_LT) {
+          const int i = e % m, j = e / m;
+          rec[L.r_S + e] = i >= j ? P[sqr_pk(i, j, m)] : 0.0;
+        }
+    }
+    for (int i = tid; i < k; i += SQR_LT) {
+      rec[L.r_l + i] = lds[L.o_l + i];
+      rec[L.r_wb + i] = lds[L.o_wb + i];
+    }
+    for (int c = tid; c < nc; c += SQR_LT) rec[L.r_mu + c] = lds[L.o_mu + c];
+  }
+  if (tid == 0) {
+    rec[L.r_st] = (double)status;
+    a.status[p] = status;
+  }
+}
+
+__device__ __forceinline__ void solve_problem_wg(Ctx& C, int64_t p, int tid) {
+  const SqrArgs& a = C.a;
+  const SqrLayout& L = C.L;
+  double* lds = C.lds;
+  const int n = a.n, m = a.m, k = a.k, nc = a.nc;
+  const double* G = a.G + p * (int64_t)k * n;
+  const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
+  const bool sing = a.sing && a.sing[p];
+  const double* rec = a.rec + p * L.rec;
+  const int status = (int)rec[L.r_st];
+  if (status != 0) {
+    const double nan = __builtin_nan("");
+    for (int i = tid; i < n; i += SQR_LT) a.cx[p * n + i] = nan;
+    for (int i = tid; i < m; i += SQR_LT) a.cy[p * m + i] = nan;
+    for (int i = tid; i < k; i += SQR_LT) {
+      a.cz[p * k + i] = nan;
+      a.cs[p * k + i] = nan;
+    }
+    if (tid == 0) a.status[p] = status;
+    return;
+  }
+  double *lam = lds + L.o_l, *wb = lds + L.o_wb, *mu = lds + L.o_mu;
+  double *dz = lds + L.o_s, *ds = lds + L.o_z;
+  double *k0 = lds + L.o_D, *k1 = lds + L.o_iW, *k2 = lds + L.o_u, *kt = lds + L.o_v;
+  double *n0 = lds + L.o_n0, *nb = lds + L.o_n1, *mv = lds + L.o_mv, *rdg = lds + L.o_nv;
+  double* P = lds + L.o_L;
+  for (int i = tid; i < k; i += SQR_LT) {
+    lam[i] = rec[L.r_l + i];
+    wb[i] = rec[L.r_wb + i];
+    dz[i] = a.dz[p * k + i];
+    ds[i] = a.ds[p * k + i];
+  }
+  for (int c = tid; c < nc; c += SQR_LT) mu[c] = rec[L.r_mu + c];
+  for (int e = tid; e < n * n; e += SQR_LT) {
+    const int i = e % n, j = e / n;
+    if (i >= j) P[sqr_pk(i, j, n)] = rec[L.r_L + e];
+  }
+  for (int j = tid; j < n; j += SQR_LT) rdg[j] = 1.0 / rec[L.r_L + (int64_t)j * n + j];
+  bar();
+  // k0 = lam \\ ds; k1 = W k0; k2 = dz - k1; k1 = W^-1 W^-1 k2   (spsolver.jl:90-96)
+  if (tid < 64)
+    for (int c = 0; c < nc; ++c) {
+      const int o = a.cones.offs[c], d = a.cones.dim[c], kd = a.cones.kind[c];
+      cone_iprod(lam, ds, k0, o, d, kd, tid);
+      cone_scale(wb, mu[c], k0, k1, o, d, kd, false, tid);
+      for (int i = o + tid; i < o + d; i += 64) k2[i] = dz[i] - k1[i];
+      cone_scale(wb, mu[c], k2, k1, o, d, kd, true, tid);
+      cone_scale(wb, mu[c], k1, k1, o, d, kd, true, tid);
+    }
+  bar();
+  // n0 = G' k1 + dx (+ A' dy)   (:97-102): a thread per column
+  for (int col = tid; col < n; col += SQR_LT) {
+    double v = dot_strided(G + (int64_t)col * k, 1, k1, k) + a.dx[p * n + col];
+    if (sing) v += dot_strided(A + (int64_t)col * m, 1, a.dy + p * m, m);
+    n0[col] = v;
+    nb[col] = v;
+  }
+  // n1 = H^-1 n0 (:104-107)
+  chol_solve_packed(P, n, rdg, nb, tid);
+  if (m > 0) {
+    // m0 = A n1 - dy; cy = S^-1 m0; m0 = sing ? dy - cy : -cy   (:108-118)
+    for (int r = tid; r < m; r += SQR_LT) mv[r] = dot_strided(A + r, m, nb, n) - a.dy[p * m + r];
+    chol_solve_global(rec + L.r_S, m, mv, tid);
+    for (int r = tid; r < m; r += SQR_LT) {
+      const double cy = mv[r], dy = a.dy[p * m + r];
+      a.cy[p * m + r] = cy;
+      mv[r] = sing ? dy - cy : -cy;
+    }
+    bar();
+    // n0 += A' m0   (:119-120)
+    for (int col = tid; col < n; col += SQR_LT) n0[col] += dot_strided(A + (int64_t)col * m, 1, mv, m);
+  }
+  // cx = H^-1 n0 (:122-124)
+  chol_solve_packed(P, n, rdg, n0, tid);
+  for (int col = tid; col < n; col += SQR_LT) a.cx[p * n + col] = n0[col];
+  // k1 = G cx - k2 (:125-126), a thread per row
+  for (int i = tid; i < k; i += SQR_LT) kt[i] = dot_strided(G + i, k, n0, n) - k2[i];
+  bar();
+  // cz = W^-1 W^-1 k1; k1 = W cz; k0 -= k1; cs = W k0   (:127-131)
+  double *cz = k2, *cs = k1;
+  if (tid < 64)
+    for (int c = 0; c < nc; ++c) {
+      const int o = a.cones.offs[c], d = a.cones.dim[c], kd = a.cones.kind[c];
+      cone_scale(wb, mu[c], kt, cz, o, d, kd, true, tid);
+      cone_scale(wb, mu[c], cz, cz, o, d, kd, true, tid);
+      cone_scale(wb, mu[c], cz, kt, o, d, kd, false, tid);
+      for (int i = o + tid; i < o + d; i += 64) k0[i] -= kt[i];
+      cone_scale(wb, mu[c], k0, cs, o, d, kd, false, tid);
+    }
+  bar();
+  for (int i = tid; i < k; i += SQR_LT) {
+    a.cz[p * k + i] = cz[i];
+    a.cs[p * k + i] = cs[i];
+  }
+  if (tid == 0) a.status[p] = 0;
+}
+
 }  // namespace
 
 template <int NC>
@@ -671,14 +1042,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void so
   solve_problem<NC>(C, (int64_t)blockIdx.x);
 }
 
-// NC = n rounded up to 16
-const void* sqr_setup_kernel_ptr(int n) {
+__global__ __launch_bounds__(SQR_LT) void socp_sqr_setup_wg_kernel(SqrArgs a) {
+  extern __shared__ double lds_dyn[];
+  const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
+  const int tid = (int)threadIdx.x;
+  Ctx C{a, L, lds_dyn, tid & 63};
+  setup_problem_wg(C, (int64_t)blockIdx.x, tid);
+}
+
+__global__ __launch_bounds__(SQR_LT) void socp_sqr_solve_wg_kernel(SqrArgs a) {
+  extern __shared__ double lds_dyn[];
+  const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
+  const int tid = (int)threadIdx.x;
+  Ctx C{a, L, lds_dyn, tid & 63};
+  solve_problem_wg(C, (int64_t)blockIdx.x, tid);
+}
+
+// NC = n rounded up to 16; the workgroup kernels above SQR_NMAX
+const void* sqr_setup_kernel_ptr(int n, int m) {
+  if (n > SQR_NMAX || m > SQR_NMAX) return (const void*)socp_sqr_setup_wg_kernel;
   if (n <= 16) return (const void*)socp_sqr_setup_kernel<16>;
   if (n <= 32) return (const void*)socp_sqr_setup_kernel<32>;
   if (n <= 48) return (const void*)socp_sqr_setup_kernel<48>;
   return (const void*)socp_sqr_setup_kernel<64>;
 }
-const void* sqr_solve_kernel_ptr(int n) {
+const void* sqr_solve_kernel_ptr(int n, int m) {
+  if (n > SQR_NMAX || m > SQR_NMAX) return (const void*)socp_sqr_solve_wg_kernel;
   if (n <= 16) return (const void*)socp_sqr_solve_kernel<16>;
   if (n <= 32) return (const void*)socp_sqr_solve_kernel<32>;
   if (n <= 48) return (const void*)socp_sqr_solve_kernel<48>;

@@ -7,28 +7,41 @@
 
 namespace socp {
 
-constexpr int SQR_NMAX = 64;   // n, m <= 64: one row per lane in the triangular solves
+constexpr int SQR_NMAX = 64;   // n, m <= 64: one row per lane in the triangular solves (wavefront kernels)
+constexpr int SQR_LMAX = 160;  // n, m <= 160: the workgroup kernels (factors packed in LDS)
 constexpr int SQR_KMAX = 256;  // k
 constexpr int SQR_KC = 8;      // G rows per LDS chunk in the H product
 constexpr int SQR_NW = 66;     // LDS row stride of a chunk (doubles; 16-byte aligned rows)
 constexpr int SQR_RHS = 8;     // right-hand sides per forward sweep in L^-1 A'
+constexpr int SQR_LT = 256;    // threads of a workgroup-kernel block (4 wavefronts)
+constexpr int SQR_RC = 16;     // right-hand sides per chunk of C = L^-1 A' (workgroup kernels)
 constexpr int SQR_CHOL_H = 2, SQR_CHOL_S = 3, SQR_DOMAIN = 4;  // include/socp.h status codes
 
 struct SqrLayout {
+  int large;     // 1: the workgroup kernels (n or m > SQR_NMAX)
   int ldl, ldm;  // LDS leading dimensions of C = L^-1 A' and L_S (odd: conflict-free row walks)
   // LDS offsets (doubles)
   int o_s, o_z, o_D, o_iW, o_u, o_v, o_l, o_wb, o_one, o_mu, o_rdgs, o_nv, o_mv, o_flag, o_X, o_S, total;
+  // workgroup kernels: the two rank-1 chains' vectors, two more n-vectors, a
+  // chunk of C, and the packed lower factor (L_H, then L_S, column-major)
+  int o_w, o_wv, o_n0, o_n1, o_C, o_L;
   // per-problem factor record (doubles): L_H (n x n, column-major, zeros above
-  // the diagonal), L_S (m x m), lambda, wb (k each), mu (nc), status
-  int64_t r_L, r_S, r_l, r_wb, r_mu, r_st, rec;
+  // the diagonal), L_S (m x m), lambda, wb (k each), mu (nc), status; the
+  // workgroup kernels add C = L^-1 A' (n x m, column-major) as scratch
+  int64_t r_L, r_S, r_l, r_wb, r_mu, r_st, r_C, rec;
 };
+
+// packed column-major lower triangle of an N x N matrix: element (i, j), i >= j
+__host__ __device__ inline int sqr_pk(int i, int j, int N) { return j * (2 * N - j + 1) / 2 + (i - j); }
 
 __host__ __device__ inline SqrLayout sqr_layout(int n, int m, int k, int nc) {
   SqrLayout L;
+  L.large = (n > SQR_NMAX || m > SQR_NMAX) ? 1 : 0;
   L.ldl = n | 1;
   L.ldm = (m > 0 ? m : 1) | 1;
   const int KP = (k + 1) / 2 * 2;
   auto ev = [](int v) { return (v + 1) / 2 * 2; };
+  const int NV = ev(n) > 64 ? ev(n) : 64, MV = ev(m) > 64 ? ev(m) : 64;
   int o = 0;
   L.o_s = o;    o += KP;
   L.o_z = o;    o += KP;
@@ -40,16 +53,28 @@ __host__ __device__ inline SqrLayout sqr_layout(int n, int m, int k, int nc) {
   L.o_wb = o;   o += KP;
   L.o_one = o;  o += KP;
   L.o_mu = o;   o += MAXC;
-  L.o_rdgs = o; o += 64;
-  L.o_nv = o;   o += 64;
-  L.o_mv = o;   o += 64;
+  L.o_rdgs = o; o += MV;
+  L.o_nv = o;   o += NV;
+  L.o_mv = o;   o += MV;
   L.o_flag = o; o += 2;
-  L.o_X = o;
-  int xs = 2 * SQR_KC * SQR_NW;          // Y row chunks (H product)
-  if (xs < 64 * 17) xs = 64 * 17;        // the H tile transpose
-  if (xs < m * L.ldl) xs = m * L.ldl;    // C = L^-1 A'
-  o += ev(xs);
-  L.o_S = o;    o += ev(m * L.ldm);
+  L.o_w = L.o_wv = L.o_n0 = L.o_n1 = L.o_C = L.o_L = 0;
+  if (!L.large) {
+    L.o_X = o;
+    int xs = 2 * SQR_KC * SQR_NW;          // Y row chunks (H product)
+    if (xs < 64 * 17) xs = 64 * 17;        // the H tile transpose
+    if (xs < m * L.ldl) xs = m * L.ldl;    // C = L^-1 A'
+    o += ev(xs);
+    L.o_S = o;    o += ev(m * L.ldm);
+  } else {
+    L.o_X = L.o_S = 0;
+    L.o_w = o;  o += NV;
+    L.o_wv = o; o += NV;
+    L.o_n0 = o; o += NV;
+    L.o_n1 = o; o += NV;
+    L.o_C = o;  o += ev(n * SQR_RC);
+    const int th = n * (n + 1) / 2, ts = m * (m + 1) / 2;
+    L.o_L = o;  o += ev(th > ts ? th : ts);
+  }
   L.total = o;
   int64_t r = 0;
   L.r_L = r;  r += (int64_t)n * n;
@@ -58,6 +83,9 @@ __host__ __device__ inline SqrLayout sqr_layout(int n, int m, int k, int nc) {
   L.r_wb = r; r += k;
   L.r_mu = r; r += nc;
   L.r_st = r; r += 1;
+  r = (r + 1) / 2 * 2;
+  L.r_C = r;
+  if (L.large) r += (int64_t)n * m;
   L.rec = (r + 1) / 2 * 2;
   return L;
 }
@@ -76,7 +104,10 @@ struct SqrArgs {
   unsigned long long* stamps;  // diagnostic build: per-phase cycle totals (setup kernel), else NULL
 };
 
-const void* sqr_setup_kernel_ptr(int n);  // instantiation for n (rounded up to 16)
-const void* sqr_solve_kernel_ptr(int n);
+// wavefront kernels for n, m <= SQR_NMAX (instantiation for n rounded up to
+// 16), workgroup kernels (SQR_LT threads) above
+const void* sqr_setup_kernel_ptr(int n, int m);
+const void* sqr_solve_kernel_ptr(int n, int m);
+inline int sqr_block_threads(int n, int m) { return (n > SQR_NMAX || m > SQR_NMAX) ? SQR_LT : 64; }
 
 }  // namespace socp

@@ -115,11 +115,15 @@ def test_host_arrays_are_size_checked():
 
 
 def test_sqr_supported_dims():
-    # the rank-update plugin: n, m <= 64, k <= 256 (socp_sqr.hpp)
+    # the rank-update plugin: n, m <= 160, k <= 256, LDS layout <= 160 KiB (socp_sqr.hpp)
     L = _lib.load()
     for name, ok in (("C0b", True), ("C1", True), ("C2", True), ("C4", False)):
         cfg = CONFIGS[name]
         d = _lib.Dims(cfg.batch, cfg.n, cfg.m, cfg.k, len(cfg.cones))
         assert bool(L.socp_sqr_supported(C.byref(d))) == ok, name
-    assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, 65, 0, 10, 1)))
+    assert L.socp_sqr_supported(C.byref(_lib.Dims(1, 65, 0, 10, 1)))
+    assert L.socp_sqr_supported(C.byref(_lib.Dims(1, 150, 102, 50, 1)))  # runtests.jl:204-244
+    assert L.socp_sqr_supported(C.byref(_lib.Dims(1, 160, 160, 256, 16)))
+    assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, 161, 0, 10, 1)))
+    assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, 64, 161, 10, 1)))
     assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, 64, 0, 257, 1)))

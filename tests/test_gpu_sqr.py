@@ -272,3 +272,105 @@ def test_sqr_shapes_vs_oracle(oracle, n, m, k, cones):
             if q:
                 ref = o[key]
                 assert np.abs(sl(got[key], q) - ref).max() <= tol * max(1.0, np.abs(ref).max()), (p, key, kap)
+
+
+def test_sqr_optimal_control_n150(oracle):
+    """The reference's own sparse-path problem (runtests.jl:204-244 'linear
+    optimal control', timed there on SparseSolver): n=150, m=102, k=50, one
+    SOC(50), G'G singular (sing: H = G'W^-2G + A'A).  Past the wavefront
+    kernels, so the workgroup kernels (factor packed in LDS) run it; iterates
+    of the oracle's rank-update IPM (F_SQR) at K = 1..4."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from problems import optimal_control
+    cones, c, A, b, G, h = optimal_control(50)
+    n, m, k = len(c), A.shape[0], G.shape[0]
+    assert oracle.sing_flag(G)
+    rng = np.random.default_rng(150)
+    for K in (1, 2, 3, 4):
+        tr = oracle.solve_trace(cones, c, A, b, G, h, params=oracle.Params(maxit=K, tol=0.0, flags=oracle.F_SQR))
+        s, z = np.asarray(tr["s"]), np.asarray(tr["z"])
+        hd = S.SqrHandle(cones, n, m, k, A.ravel(order="F"), G.ravel(order="F"), np.ones(1, np.uint8))
+        st = hd.setup_iter(s, z)
+        r = [rng.standard_normal(q) for q in (n, m, k, k)]
+        got = hd.solve_kkt(*r)
+        o = oracle.sqr_kkt_single(cones, A, G, True, s, z, *r)
+        assert st[0] == o["status"] == 0, (K, st[0], o["status"])
+        assert S.default_context().last_kernel_name() == "socp_sqr_solve_wg_kernel"
+        assert np.abs(np.tril(hd.factor(0)) - o["L"]).max() <= 1e-9 * np.abs(o["L"]).max(), K
+        Hm = o["L"] @ o["L"].T
+        kap = np.linalg.cond(Hm) * np.linalg.cond(A @ np.linalg.solve(Hm, A.T))
+        tol = max(1e-9, 1e-15 * kap)
+        for key in ("cx", "cy", "cz", "cs"):
+            ref = o[key]
+            assert np.abs(got[key] - ref).max() <= tol * max(1.0, np.abs(ref).max()), (K, key, kap)
+
+
+@pytest.mark.parametrize("n,m,k,cones,sing", [
+    (100, 30, 120, [(0, 0, 40), (1, 40, 80)], False),               # n > 64
+    (70, 66, 100, [(1, 0, 50), (1, 50, 50)], True),                 # m > 64: sing, A'A in H
+    (160, 160, 256, [(0, 0, 16)] + [(1, 16 + 16 * i, 16) for i in range(15)], True),  # n, m, k at their limits
+    (77, 0, 90, [(1, 0, 30), (1, 30, 29), (1, 59, 31)], False),     # ragged SOC cones, m = 0
+    (129, 65, 140, [(0, 0, 140)], False),                           # LP: no modification, odd sizes
+])
+def test_sqr_workgroup_shapes_vs_oracle(oracle, n, m, k, cones, sing):
+    rng = np.random.default_rng(n * 1000 + m * 10 + k)
+    B = 6
+    G = rng.standard_normal((B, k, n))
+    if sing:
+        G[:, :, n // 2:] = 0.0  # G'G singular: the A'A term carries H
+    A = rng.standard_normal((B, m, n))
+    s, z = _interior(rng, cones, B, k), _interior(rng, cones, B, k)
+    Gf = np.concatenate([G[p].ravel(order="F") for p in range(B)])
+    Af = np.concatenate([A[p].ravel(order="F") for p in range(B)]) if m else None
+    h = S.SqrHandle(cones, n, m, k, Af, Gf, np.full(B, 1 if sing else 0, np.uint8))
+    st = h.setup_iter(s.ravel(), z.ravel())
+    r = [rng.standard_normal(B * q) for q in (n, m, k, k)]
+    got = h.solve_kkt(r[0], r[1] if m else None, r[2], r[3])
+    assert S.default_context().last_kernel_name() == "socp_sqr_solve_wg_kernel"
+    ok = 0
+    for p in range(B):
+        sl = lambda v, q: v[p * q:(p + 1) * q]  # noqa: E731
+        o = oracle.sqr_kkt_single(cones, A[p], G[p], sing, s[p], z[p], sl(r[0], n), sl(r[1], m), sl(r[2], k),
+                                  sl(r[3], k))
+        assert st[p] == o["status"], p
+        if o["status"]:
+            assert np.isnan(sl(got["cx"], n)).all()
+            continue
+        ok += 1
+        assert np.abs(np.tril(h.factor(p)) - o["L"]).max() <= 1e-9 * np.abs(o["L"]).max(), p
+        Hm = o["L"] @ o["L"].T
+        kap = np.linalg.cond(Hm) * (np.linalg.cond(A[p] @ np.linalg.solve(Hm, A[p].T)) if m else 1.0)
+        tol = max(1e-9, 1e-15 * kap)
+        for key, q in (("cx", n), ("cy", m), ("cz", k), ("cs", k)):
+            if q:
+                ref = o[key]
+                assert np.abs(sl(got[key], q) - ref).max() <= tol * max(1.0, np.abs(ref).max()), (p, key, kap)
+    assert ok >= B // 2
+
+
+def test_sqr_workgroup_failures_isolated(oracle):
+    """A domain error and a lost downdate in one problem of a workgroup-kernel
+    batch leave its neighbours bit-identical."""
+    rng = np.random.default_rng(11)
+    n, m, k, B = 90, 20, 100, 5
+    cones = [(0, 0, 20), (1, 20, 80)]
+    G = rng.standard_normal((B, k, n))
+    A = rng.standard_normal((B, m, n))
+    s, z = _interior(rng, cones, B, k), _interior(rng, cones, B, k)
+    Gf = np.concatenate([G[p].ravel(order="F") for p in range(B)])
+    Af = np.concatenate([A[p].ravel(order="F") for p in range(B)])
+    r = [rng.standard_normal(B * q) for q in (n, m, k, k)]
+    clean = S.SqrHandle(cones, n, m, k, Af, Gf, np.zeros(B, np.uint8))
+    assert (clean.setup_iter(s.ravel(), z.ravel()) == 0).all()
+    ref = clean.solve_kkt(*r)
+    s2 = s.copy()
+    s2[2, 30] = 50.0  # problem 2: SOC tail above its head -> sqrt of a negative
+    bad = S.SqrHandle(cones, n, m, k, Af, Gf, np.zeros(B, np.uint8))
+    st = bad.setup_iter(s2.ravel(), z.ravel())
+    assert st[2] == S.DOMAIN_ERROR and (st[[0, 1, 3, 4]] == 0).all()
+    out = bad.solve_kkt(*r)
+    assert np.isnan(out["cx"][2 * n:3 * n]).all()
+    for p in (0, 1, 3, 4):
+        assert np.array_equal(out["cx"][p * n:(p + 1) * n], ref["cx"][p * n:(p + 1) * n])
