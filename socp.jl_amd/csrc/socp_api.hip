@@ -907,6 +907,9 @@ extern "C" int socp_sqr_create(socp_ctx* ctx, const socp_dims* dims, const int32
   if (h->buf[Q::Q_REC].ensure((size_t)B * (size_t)h->L.rec * sizeof(double)))
     return bail(fail(SOCP_E_NOMEM, "factor record allocation failed"));
   a.rec = (double*)h->buf[Q::Q_REC].p;
+  // the setup kernels write only the factors' lower triangles
+  if (hipMemsetAsync(a.rec, 0, (size_t)B * (size_t)h->L.rec * sizeof(double), ctx->stream) != hipSuccess)
+    return bail(fail(SOCP_E_HIP, "hipMemsetAsync"));
   const void* kerns[2] = {sqr_setup_kernel_ptr(n, m), sqr_solve_kernel_ptr(n, m)};
   for (const void* kern : kerns)
     if (h->lds > 64 * 1024 &&

@@ -335,6 +335,35 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
   int status = (int)lds[L.o_flag];
   double h[NC];
   double rd = lane >= n ? 1.0 : 0.0;  // lane j: 1 / L(j,j) (1 on the identity-padded rows)
+  // modify_factors!' G'u and G'v (sqrscalings.jl:160-194) of the first (up to 8)
+  // SOC cones ride along the H product as one more 16-row MFMA operand (slot
+  // j = 2 c' + {0: u, 1: v} of SOC cone c'), against the G row chunks already
+  // staged in LDS -- no second pass over G.  The results land in the s..v
+  // vectors' LDS (dead after the product: 6 KP doubles), so when they do not
+  // fit, or (non-sing) a SOC row's iW is 0 (the staged rows are iW G, the
+  // weights u / iW), the cones are re-read from G below.
+  int c_soc = 0;
+  while (c_soc < nc && a.cones.kind[c_soc] != SOC_K) ++c_soc;
+  const int fslots = (nc - c_soc) < 8 ? (nc - c_soc) : 8;
+  double* wuv = lds + L.o_s;  // wuv[j * n + col], j < 2 fslots: over s, z, D, iW (u, v stay for the re-read cones)
+  bool fuse = status == 0 && fslots > 0 && 2 * fslots * n <= 4 * ((k + 1) / 2 * 2);
+  // rows of the fused cones (contiguous): [fr0, fr1)
+  const int fr0 = fslots > 0 ? a.cones.offs[c_soc] : 0;
+  const int fr1 = fslots > 0 ? a.cones.offs[c_soc + fslots - 1] + a.cones.dim[c_soc + fslots - 1] : 0;
+  if (fuse && !sing) {
+    bool zero = false;
+    for (int i = fr0 + lane; i < fr1; i += 64) zero |= !(lds[L.o_iW + i] > 0.0);
+    fuse = !__any(zero);
+    if (fuse) {
+      wsync();
+      for (int i = fr0 + lane; i < fr1; i += 64) {
+        const double iw = lds[L.o_iW + i];
+        lds[L.o_u + i] /= iw;
+        lds[L.o_v + i] /= iw;
+      }
+      wsync();
+    }
+  }
   if (status == 0) {
     // ---- H = G'DG (+A'A) on f64 MFMA 16x16x4: the lower 16x16 tiles,
     // Y rows staged through LDS 8 at a time; then one LDS transpose gives each
@@ -346,6 +375,14 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
     d4v acc[NT * (NT + 1) / 2];
 #pragma unroll
     for (int t = 0; t < NT * (NT + 1) / 2; ++t) acc[t] = d4v{0.0, 0.0, 0.0, 0.0};
+    d4v accx[NT];  // (w_j' G)[16X + col] of the fused G'u / G'v
+#pragma unroll
+    for (int t = 0; t < NT; ++t) accx[t] = d4v{0.0, 0.0, 0.0, 0.0};
+    // this lane's weight slot: SOC cone c_soc + (lane & 15) / 2, u or v
+    const int wslot = (lane & 15) >> 1;
+    const int wo = wslot < fslots ? a.cones.offs[c_soc + wslot] : 0;
+    const int we = wslot < fslots ? wo + a.cones.dim[c_soc + wslot] : 0;
+    const double* wvec = lds + ((lane & 1) ? L.o_v : L.o_u);
     double *Ya = lds + L.o_X, *Yb = Ya + SQR_KC * SQR_NW;
     // non-sing: (iW G)'(iW G) (spsolver.jl:62-64); sing: G'(iWiW G) + A'A (:67-71)
     const double *fa = lds + (sing ? L.o_one : L.o_iW), *fb = lds + (sing ? L.o_D : L.o_iW);
@@ -391,8 +428,25 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
           for (int I = 0; I < NT; ++I)
 #pragma unroll
             for (int J = 0; J <= I; ++J, ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[I], bv[J], acc[t], 0, 0, 0);
+          if (fuse && pass == 0) {
+            const int row = r0 + rr;
+            const double wt = (row >= wo && row < we) ? wvec[row] : 0.0;
+#pragma unroll
+            for (int X = 0; X < NT; ++X) accx[X] = __builtin_amdgcn_mfma_f64_16x16x4f64(wt, av[X], accx[X], 0, 0, 0);
+          }
         }
       }
+    }
+    if (fuse) {
+      wsync();  // every lane is past the product's reads of s..v
+#pragma unroll
+      for (int X = 0; X < NT; ++X)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int j = (lane >> 4) + 4 * v, col = 16 * X + (lane & 15);
+          if (j < 2 * fslots && col < n) wuv[j * n + col] = accx[X][v];
+        }
+      wsync();
     }
     {
       double* T = lds + L.o_X;  // 64 x 17 staging of one 16-column block
@@ -453,7 +507,11 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
       double w[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        if (lane < n && 2 * q < nch) {
+        const int slot = c0 + q - c_soc;
+        if (lane < n && 2 * q < nch && fuse && slot < fslots) {  // from the fused product
+          w[2 * q] = wuv[2 * slot * n + lane];
+          w[2 * q + 1] = wuv[(2 * slot + 1) * n + lane];
+        } else if (lane < n && 2 * q < nch) {
           const int o = a.cones.offs[c0 + q], d = a.cones.dim[c0 + q];
           for (int r = o; r < o + d; ++r) {
             const double g = G[(int64_t)lane * k + r];
@@ -511,9 +569,11 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
   }
   // ---- the factor record
   if (status == 0) {
+    // the lower triangle only: the record's upper triangle is zeroed once by
+    // socp_sqr_create and never written
 #pragma unroll
     for (int j = 0; j < NC; ++j)
-      if (j < n && lane < n) rec[L.r_L + j * n + lane] = lane >= j ? h[j] : 0.0;
+      if (j < n && lane < n && lane >= j) rec[L.r_L + j * n + lane] = h[j];
     wsync();
     const double* Sm = lds + L.o_S;
     for (int e = lane; e < m * m; e += 64) {
@@ -874,9 +934,9 @@ __device__ __forceinline__ void setup_problem_wg(Ctx& C, int64_t p, int tid) {
   if (status == 0) {
     for (int j = tid; j < n; j += SQR_LT) rdg[j] = 1.0 / P[sqr_pk(j, j, n)];
     // the factor into the record (column-major, zeros above the diagonal)
-    for (int e = tid; e < n * n; e += SQR_LT) {
+    for (int e = tid; e < n * n; e += SQR_LT) {  // lower triangle (the upper one stays zero)
       const int i = e % n, j = e / n;
-      rec[L.r_L + e] = i >= j ? P[sqr_pk(i, j, n)] : 0.0;
+      if (i >= j) rec[L.r_L + e] = P[sqr_pk(i, j, n)];
     }
     bar();
     if (m > 0) {
@@ -1026,8 +1086,10 @@ __device__ __forceinline__ void solve_problem_wg(Ctx& C, int64_t p, int tid) {
 
 }  // namespace
 
+// NC = 64: the LDS layout (~20 KB at the C2 shape) admits 8 workgroups per
+// CU, i.e. 2 waves per SIMD, so the register budget is 256 (no spills)
 template <int NC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void socp_sqr_setup_kernel(SqrArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC >= 64 ? 2 : 3))) void socp_sqr_setup_kernel(SqrArgs a) {
   extern __shared__ double lds_dyn[];
   const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
   Ctx C{a, L, lds_dyn, (int)threadIdx.x};
@@ -1035,7 +1097,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void so
 }
 
 template <int NC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void socp_sqr_solve_kernel(SqrArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC >= 64 ? 2 : 3))) void socp_sqr_solve_kernel(SqrArgs a) {
   extern __shared__ double lds_dyn[];
   const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
   Ctx C{a, L, lds_dyn, (int)threadIdx.x};

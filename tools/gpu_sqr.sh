@@ -6,7 +6,7 @@ set -e
 export TMPDIR=/tmp
 O=gpurun_out/sqr
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_sqr.py -x -v --timeout 120 --timeout-method thread > $O/pytest_sqr.log 2>&1 || { tail -60 $O/pytest_sqr.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_sqr.py -x -q --tb=line --timeout 120 --timeout-method thread > $O/pytest_sqr.log 2>&1 || { tail -60 $O/pytest_sqr.log; exit 1; }
 tail -3 $O/pytest_sqr.log
 if [ -z "$NO_PMC" ]; then
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f -o f -- python3 bench.py --mode sqr --steps 1 --warmup 0 --no-cpu > $O/pmc_f.log 2>&1 || { tail -20 $O/pmc_f.log; exit 1; }
