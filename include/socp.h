@@ -243,6 +243,19 @@ int socp_sqr_solve_kkt(socp_sqr* h, const double* dx, const double* dy, const do
                        int32_t* status);
 int socp_sqr_factor(socp_sqr* h, int64_t problem, double* L);
 int socp_sqr_scaling(socp_sqr* h, double* l, double* wbs, double* mu);
+/* solve_socp(prob, SolverState(prob, SparseSolver(prob))) (solver.jl:40-153)
+ * for the handle's whole batch -- the reference's own tested configuration
+ * (runtests.jl:143-144, 188-189, 204-244) -- with this plugin's setup_iter /
+ * solve_kkt: initial point (the KKT system with W = I and the cone shift,
+ * solver.jl:68-104), then up to params->maxit iterations with the reference's
+ * exit test, per-problem status and masking (problems that stop are skipped by
+ * every later launch).  c (B x n), b (B x m), h (B x k) in; x, y, z, s, iters,
+ * status, res (B x 3: ||rd||, ||rp||, z's at the returned iterate; may be
+ * NULL) out.  params NULL: socp_params_default.  Host or device pointers as
+ * the handle's flags.  Afterwards the records hold the last factorisation. */
+int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b, const double* hvec,
+                        const socp_params* params, double* x, double* y, double* z, double* s,
+                        int32_t* iters, int32_t* status, double* res);
 int socp_sqr_h2d_bytes(const socp_sqr* h, int64_t* bytes);
 int64_t socp_sqr_record_bytes(const socp_sqr* h);
 int socp_sqr_destroy(socp_sqr* h);

@@ -810,8 +810,9 @@ struct socp_sqr {
   size_t lds = 0;
   bool dev = false, ready = false;
   int64_t h2d_bytes = 0;
+  int deg = 0;  // deg(cones) (vectors.jl:165-179), for mu = lam'lam / deg in solve_socp
   enum { Q_A, Q_G, Q_SING, Q_REC, Q_S, Q_Z, Q_DX, Q_DY, Q_DZ, Q_DS, Q_CX, Q_CY, Q_CZ, Q_CS, Q_ST, Q_OUT,
-         NQB };
+         Q_IPM, NQB };
   DevBuf buf[NQB];
 };
 
@@ -872,6 +873,7 @@ extern "C" int socp_sqr_create(socp_ctx* ctx, const socp_dims* dims, const int32
   int degree = 0;
   int rc = check_problem(dims, cone_kind, cone_offs, cone_dim, &a.cones, &degree);
   if (rc) return bail(rc);
+  h->deg = degree;
   if (!sqr_fits(dims, &h->lds))
     return bail(fail(SOCP_E_UNSUPPORTED, "rank-update plugin: n, m <= 160, k <= 256, LDS layout <= 160 KiB (socp_sqr.hip)"));
   const int64_t B = dims->batch;
@@ -927,16 +929,16 @@ extern "C" int socp_sqr_destroy(socp_sqr* h) {
   return 0;
 }
 
-static int sqr_launch(socp_sqr* h, const SqrArgs& a, bool setup) {
+static int sqr_launch(socp_sqr* h, const SqrArgs& a, bool setup, bool timed = true) {
   socp_ctx* ctx = h->ctx;
   const void* kern = setup ? sqr_setup_kernel_ptr(a.n, a.m) : sqr_solve_kernel_ptr(a.n, a.m);
   SqrArgs la = a;
   la.stamps = g_stamps;
   void* kargs[] = {&la};
-  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  if (timed) HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
   const int nt = sqr_block_threads(a.n, a.m);
   HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(nt), kargs, h->lds, ctx->stream));
-  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  if (timed) HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
   ctx->last_name = nt > 64 ? (setup ? "socp_sqr_setup_wg_kernel" : "socp_sqr_solve_wg_kernel")
                            : (setup ? "socp_sqr_setup_kernel" : "socp_sqr_solve_kernel");
   return 0;
@@ -999,6 +1001,125 @@ extern "C" int socp_sqr_solve_kkt(socp_sqr* h, const double* dx, const double* d
   TRY(copy_back(ctx, cs, a.cs, (size_t)B * k, h->dev));
   TRY(copy_back(ctx, status, a.status, (size_t)B, h->dev));
   if (!h->dev) HIPCHK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+// solve_socp(prob, SolverState(prob, SparseSolver(prob))) (solver.jl:40-153)
+// for the handle's whole batch: the initial point, then up to maxit iterations
+// of setup_iter + two solve_kkt with this plugin, every problem masked out of
+// the launches once it stops (socp_sqr_ipm.hip).  c, b, h in; x, y, z, s,
+// iters, status (and res: ||rd||, ||rp||, z's at the returned iterate, may be
+// NULL) out; host or device pointers as the handle's flags say.
+extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b, const double* hv,
+                                   const socp_params* params, double* x, double* y, double* z, double* s,
+                                   int32_t* iters, int32_t* status, double* res) {
+  if (!h) return fail(SOCP_E_INVALID, "handle is NULL");
+  const int64_t B = h->a.B;
+  if (B == 0) return 0;
+  const int n = h->a.n, m = h->a.m, k = h->a.k;
+  if (!c || !hv || !x || !z || !s || !iters || !status || (m > 0 && (!b || !y)))
+    return fail(SOCP_E_INVALID, "NULL data pointer");
+  socp_params P;
+  if (params) P = *params; else socp_params_default(&P);
+  if (P.maxit < 0) return fail(SOCP_E_INVALID, "maxit < 0");
+  socp_ctx* ctx = h->ctx;
+  HIPCHK(hipSetDevice(ctx->device));
+  h->h2d_bytes = 0;
+  // device block: c b h | x y z s | dx dy dz ds | rx ry rz rs | res | status iters active st_setup st_solve
+  const size_t nd = (size_t)B * (n + m + k) + 4 * (size_t)B * (n + m + 2 * k) + 3 * (size_t)B;
+  const size_t ni = 5 * (size_t)B;
+  typedef socp_sqr Q;
+  if (h->buf[Q::Q_IPM].ensure(nd * sizeof(double) + ni * sizeof(int32_t)))
+    return fail(SOCP_E_NOMEM, "device allocation failed");
+  double* d = (double*)h->buf[Q::Q_IPM].p;
+  SqrIpmArgs ia;
+  memset(&ia, 0, sizeof(ia));
+  ia.B = B; ia.n = n; ia.m = m; ia.k = k; ia.nc = h->a.nc; ia.deg = h->deg; ia.sigma_exp = P.sigma_exp;
+  ia.cones = h->a.cones;
+  ia.A = h->a.A; ia.G = h->a.G;
+  double* dc = d;
+  double* db = dc + (size_t)B * n;
+  double* dh = db + (size_t)B * m;
+  double* q = dh + (size_t)B * k;
+  auto carve4 = [&](double** o0, double** o1, double** o2, double** o3) {
+    *o0 = q; q += (size_t)B * n;
+    *o1 = q; q += (size_t)B * m;
+    *o2 = q; q += (size_t)B * k;
+    *o3 = q; q += (size_t)B * k;
+  };
+  carve4(&ia.x, &ia.y, &ia.z, &ia.s);
+  carve4(&ia.dx, &ia.dy, &ia.dz, &ia.ds);
+  carve4(&ia.rx, &ia.ry, &ia.rz, &ia.rs);
+  ia.res = q; q += 3 * (size_t)B;
+  int32_t* ip = (int32_t*)q;
+  ia.status = ip; ia.iters = ip + B; ia.active = ip + 2 * B; ia.st_setup = ip + 3 * B;
+  int32_t* st_solve = ip + 4 * B;
+  const bool dev = h->dev;
+  if (dev) {
+    ia.c = c; ia.b = m ? b : nullptr; ia.h = hv;
+  } else {
+    HIPCHK(hipMemcpyAsync(dc, c, (size_t)B * n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    if (m) HIPCHK(hipMemcpyAsync(db, b, (size_t)B * m * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(dh, hv, (size_t)B * k * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    h->h2d_bytes += (int64_t)((size_t)B * (n + m + k) * sizeof(double));
+    ia.c = dc; ia.b = db; ia.h = dh;
+  }
+  ia.rec = h->a.rec; ia.rec_stride = h->L.rec; ia.r_l = h->L.r_l; ia.r_wb = h->L.r_wb; ia.r_mu = h->L.r_mu;
+  ia.tol = P.tol; ia.step = P.step; ia.init_eps = P.init_eps;
+  // the plugin's own launches on the IPM's buffers
+  SqrArgs su = h->a;  // setup_iter(s, z)
+  su.s = ia.s; su.z = ia.z; su.status = ia.st_setup; su.active = nullptr;
+  SqrArgs sv = h->a;  // solve_kkt(dx, dy, dz, ds) -> (rx, ry, rz, rs)
+  sv.dx = ia.dx; sv.dy = ia.dy; sv.dz = ia.dz; sv.ds = ia.ds;
+  sv.cx = ia.rx; sv.cy = ia.ry; sv.cz = ia.rz; sv.cs = ia.rs; sv.status = st_solve; sv.active = nullptr;
+  const size_t lds = sqr_ipm_lds_bytes(n, m, k);
+  const dim3 grid((unsigned)B), blk(64);
+  auto ipm = [&](int which, int it) -> int {
+    void* args1[] = {&ia};
+    void* args2[] = {&ia, &it};
+    HIPCHK(hipLaunchKernel(sqr_ipm_kernel_ptr(which), grid, blk, which == 4 ? args2 : args1, lds, ctx->stream));
+    return 0;
+  };
+  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  // initial point: the KKT system with W = I (s = z = e), then the shift
+  TRY(ipm(0, 0));
+  TRY(sqr_launch(h, su, true, false));
+  sv.init = 1;
+  TRY(sqr_launch(h, sv, false, false));
+  sv.init = 0;
+  TRY(ipm(1, 0));
+  su.active = ia.active;
+  sv.active = ia.active;
+  for (int it = 0; it < P.maxit; ++it) {
+    TRY(sqr_launch(h, su, true, false));   // compute_scaling + setup_iter
+    TRY(ipm(2, it));                       // residuals, exit test, affine right-hand side
+    TRY(sqr_launch(h, sv, false, false));  // solve_kkt (affine)
+    TRY(ipm(3, it));                       // step, sigma, mu, corrector right-hand side
+    TRY(sqr_launch(h, sv, false, false));  // solve_kkt (combined)
+    TRY(ipm(4, it));                // step and update
+  }
+  if (res) TRY(ipm(5, 0));
+  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  ctx->last_name = "socp_sqr_solve_socp";
+  if (dev) {
+    HIPCHK(hipMemcpyAsync(x, ia.x, (size_t)B * n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    if (m) HIPCHK(hipMemcpyAsync(y, ia.y, (size_t)B * m * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(z, ia.z, (size_t)B * k * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(s, ia.s, (size_t)B * k * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(iters, ia.iters, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(status, ia.status, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, ctx->stream));
+    if (res) HIPCHK(hipMemcpyAsync(res, ia.res, 3 * (size_t)B * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+  } else {
+    TRY(copy_back(ctx, x, (const double*)ia.x, (size_t)B * n, false));
+    if (m) TRY(copy_back(ctx, y, (const double*)ia.y, (size_t)B * m, false));
+    TRY(copy_back(ctx, z, (const double*)ia.z, (size_t)B * k, false));
+    TRY(copy_back(ctx, s, (const double*)ia.s, (size_t)B * k, false));
+    TRY(copy_back(ctx, iters, (const int32_t*)ia.iters, (size_t)B, false));
+    TRY(copy_back(ctx, status, (const int32_t*)ia.status, (size_t)B, false));
+    if (res) TRY(copy_back(ctx, res, (const double*)ia.res, 3 * (size_t)B, false));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  h->ready = true;  // the records hold the last iteration's factorisation
   return 0;
 }
 

@@ -319,6 +319,7 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
   const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
   const bool sing = a.sing && a.sing[p];
   double* rec = a.rec + p * L.rec;
+  if (a.active && !a.active[p]) return;
 #ifdef SOCP_DIAG
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -605,6 +606,7 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
   const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
   const bool sing = a.sing && a.sing[p];
   const double* rec = a.rec + p * L.rec;
+  if (a.active && !a.active[p]) return;
   const int status = (int)rec[L.r_st];
   if (status != 0) {
     const double nan = __builtin_nan("");
@@ -677,7 +679,7 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
     if (lane < m) {
       a.cy[p * m + lane] = cy;
       const double dy = a.dy[p * m + lane];
-      mv[lane] = sing ? dy - cy : -cy;
+      mv[lane] = (sing && !a.init) ? dy - cy : -cy;  // init: the exact KKT solution (solver.jl:84)
     }
     wsync();
     // n0 += A' m0   (:119-120)
@@ -844,6 +846,7 @@ __device__ __forceinline__ void setup_problem_wg(Ctx& C, int64_t p, int tid) {
   const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
   const bool sing = a.sing && a.sing[p];
   double* rec = a.rec + p * L.rec;
+  if (a.active && !a.active[p]) return;  // uniform over the workgroup
   double* P = lds + L.o_L;
   double* rdg = lds + L.o_nv;  // 1 / diag of the current factor
   for (int i = tid; i < k; i += SQR_LT) {
@@ -996,6 +999,7 @@ __device__ __forceinline__ void solve_problem_wg(Ctx& C, int64_t p, int tid) {
   const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
   const bool sing = a.sing && a.sing[p];
   const double* rec = a.rec + p * L.rec;
+  if (a.active && !a.active[p]) return;  // uniform over the workgroup
   const int status = (int)rec[L.r_st];
   if (status != 0) {
     const double nan = __builtin_nan("");
@@ -1053,7 +1057,7 @@ __device__ __forceinline__ void solve_problem_wg(Ctx& C, int64_t p, int tid) {
     for (int r = tid; r < m; r += SQR_LT) {
       const double cy = mv[r], dy = a.dy[p * m + r];
       a.cy[p * m + r] = cy;
-      mv[r] = sing ? dy - cy : -cy;
+      mv[r] = (sing && !a.init) ? dy - cy : -cy;  // init: the exact KKT solution (solver.jl:84)
     }
     bar();
     // n0 += A' m0   (:119-120)

@@ -102,7 +102,28 @@ struct SqrArgs {
   int32_t* status;         // B
   double* rec;             // B x rec
   unsigned long long* stamps;  // diagnostic build: per-phase cycle totals (setup kernel), else NULL
+  const int32_t* active;   // B or NULL: problems with active[p] == 0 are skipped (the batched IPM's mask)
+  int32_t init;            // solve: the initial-point system (solver.jl:68-84, an exact solve in the
+                           // reference): m0 = -cy also when sing, as the dense kernel's MP_INIT
 };
+
+// the batched solve_socp on the rank-update plugin (socp_sqr_ipm.hip): the
+// state, right-hand sides and KKT solutions of every problem, per-problem
+// status / iteration count / activity, the setup launch's status
+struct SqrIpmArgs {
+  int64_t B;
+  int n, m, k, nc, deg, sigma_exp;
+  ConeTable cones;
+  const double *A, *G, *c, *b, *h;
+  const double* rec;  // the plugin's factor records: lambda, wb, mu at r_l, r_wb, r_mu
+  int64_t rec_stride, r_l, r_wb, r_mu;
+  double *x, *y, *z, *s, *dx, *dy, *dz, *ds, *rx, *ry, *rz, *rs, *res;
+  int32_t *status, *iters, *active, *st_setup;
+  double tol, step, init_eps;
+};
+size_t sqr_ipm_lds_bytes(int n, int m, int k);
+// 0 init, 1 shift, 2 resid, 3 step1, 4 step2 (extra int argument: the iteration), 5 final
+const void* sqr_ipm_kernel_ptr(int which);
 
 // wavefront kernels for n, m <= SQR_NMAX (instantiation for n rounded up to
 // 16), workgroup kernels (SQR_LT threads) above

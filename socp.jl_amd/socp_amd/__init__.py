@@ -351,6 +351,38 @@ class SqrHandle(DenseHandle):
         _lib.check(self._fn("factor")(self.handle, int(problem), _lib.ptr(out)))
         return out.reshape(self.n, self.n, order="F")
 
+    def solve_socp(self, c, b, h, *, maxit=40, tol=1e-5, step=0.99, sigma_exp=3, init_eps=1e-10, res=True):
+        """solve_socp(prob, SolverState(prob, SparseSolver(prob))) (solver.jl:40-153)
+        for every problem of the batch, on this plugin (socp_sqr_solve_socp):
+        the reference's own tested path, batched.  Returns dict(x, y, z, s,
+        iters, status[, res]) like ``batch_solve``; numpy or torch as the handle."""
+        B, n, m, k = self.B, self.n, self.m, self.k
+        _check_sizes(B, c=(c, B * n), b=(b if m else None, B * m), h=(h, B * k))
+        if self.dev:
+            import torch
+            dv = c.device
+            f64 = dict(dtype=torch.float64, device=dv)
+            out = dict(x=torch.empty(B * n, **f64), y=torch.empty(max(B * m, 1), **f64),
+                       z=torch.empty(B * k, **f64), s=torch.empty(B * k, **f64),
+                       iters=torch.empty(B, dtype=torch.int32, device=dv),
+                       status=torch.empty(B, dtype=torch.int32, device=dv))
+            if res:
+                out["res"] = torch.empty(3 * B, **f64)
+            self.ctx.bind_torch_stream()
+        else:
+            out = dict(x=np.zeros(B * n), y=np.zeros(max(B * m, 1)), z=np.zeros(B * k), s=np.zeros(B * k),
+                       iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32))
+            if res:
+                out["res"] = np.zeros(3 * B)
+        P = _lib.default_params(maxit=maxit, tol=tol, step=step, sigma_exp=sigma_exp, init_eps=init_eps)
+        p = _lib.ptr
+        _lib.check(self._fn("solve_socp")(self.handle, p(self._arg(c)), p(self._arg(b)) if m else None,
+                                           p(self._arg(h)), C.byref(P), p(out["x"]), p(out["y"]) if m else None,
+                                           p(out["z"]), p(out["s"]), p(out["iters"]), p(out["status"]),
+                                           p(out.get("res"))))
+        out["y"] = out["y"][:B * m]
+        return out
+
     def scaling(self):
         """dict(l, wbs, mu) of the last setup_iter for every problem (host arrays
         B x k, B x k, B x ncones): the SqrScaling fields the driver loop reads."""
@@ -647,9 +679,9 @@ class SparseSolver(DenseSolver):
     rank-update path -- G'DG factored, one rank-1 update and one downdate per
     SOC cone, triangular solves (a one-problem SqrHandle).  The reference runs
     it through CHOLMOD; here the factor is dense and LDS-resident.  The plugin
-    methods are setup_iter / solve_kkt; the whole-batch device solver
-    (solve_socp) runs the dense elimination, which computes the same KKT
-    solutions to rounding."""
+    methods are setup_iter / solve_kkt; solve_socp with this plugin runs the
+    reference's IPM loop on the device with these same kernels
+    (SqrHandle.solve_socp, socp_sqr_solve_socp)."""
 
     scaling_type = SqrScaling
 
@@ -709,18 +741,23 @@ class SolverState:
 def solve_socp(prob: Problem, ss: SolverState) -> State:
     """solve_socp(prob, ss) (solver.jl:40-153) on the GPU.  Like the reference it
     returns the final State, and raises where the reference throws."""
-    out = batch_solve(prob.cones, prob.n, prob.m, prob.k, prob.c, _colmajor(prob.A, prob.m, prob.n),
-                      prob.b, _colmajor(prob.G, prob.k, prob.n), prob.h,
-                      np.array([prob.sing], np.uint8), maxit=ss.maxit, tol=ss.tol,
-                      ctx=ss.solver.ctx)
+    if isinstance(ss.solver, SparseSolver):  # the rank-update plugin's own IPM (spsolver.jl)
+        out = ss.solver.handle.solve_socp(prob.c, prob.b if prob.m else None, prob.h, maxit=ss.maxit, tol=ss.tol)
+    else:
+        out = batch_solve(prob.cones, prob.n, prob.m, prob.k, prob.c, _colmajor(prob.A, prob.m, prob.n),
+                          prob.b, _colmajor(prob.G, prob.k, prob.n), prob.h,
+                          np.array([prob.sing], np.uint8), maxit=ss.maxit, tol=ss.tol,
+                          ctx=ss.solver.ctx)
     ss.iters, ss.status = int(out["iters"][0]), int(out["status"][0])
     _raise_status(ss.status)
     return State(prob, out["x"], out["y"], out["z"], out["s"])
 
 
-def solve_socp_batched(problems, maxit=40, tol=1e-5, ctx=None):
+def solve_socp_batched(problems, maxit=40, tol=1e-5, ctx=None, solver="dense"):
     """Batched solve of Problems sharing dims and cones; returns (states, iters, status)
-    without raising: failures are reported per problem."""
+    without raising: failures are reported per problem.  solver="dense": the
+    DenseSolver path (the fused register / blocked kernels); "sqr": the
+    SparseSolver rank-update path (SqrHandle.solve_socp)."""
     p0 = problems[0]
     n, m, k = p0.n, p0.m, p0.k
     for p in problems:
@@ -731,7 +768,10 @@ def solve_socp_batched(problems, maxit=40, tol=1e-5, ctx=None):
     G = np.concatenate([_colmajor(p.G, k, n) for p in problems])
     h = np.concatenate([p.h for p in problems])
     sing = np.array([p.sing for p in problems], np.uint8)
-    out = batch_solve(p0.cones, n, m, k, c, A, b, G, h, sing, maxit=maxit, tol=tol, ctx=ctx)
+    if solver == "sqr":
+        out = SqrHandle(p0.cones, n, m, k, A, G, sing, ctx=ctx).solve_socp(c, b, h, maxit=maxit, tol=tol)
+    else:
+        out = batch_solve(p0.cones, n, m, k, c, A, b, G, h, sing, maxit=maxit, tol=tol, ctx=ctx)
     states = [State(p, out["x"][i * n:(i + 1) * n], out["y"][i * m:(i + 1) * m],
                     out["z"][i * k:(i + 1) * k], out["s"][i * k:(i + 1) * k])
               for i, p in enumerate(problems)]

@@ -33,6 +33,7 @@ EXPORTED = [
     "socp_ingest_wait", "socp_ingest_destroy",
     "socp_sqr_supported", "socp_sqr_create", "socp_sqr_setup_iter", "socp_sqr_solve_kkt", "socp_sqr_factor",
     "socp_sqr_scaling", "socp_sqr_h2d_bytes", "socp_sqr_record_bytes", "socp_sqr_destroy",
+    "socp_sqr_solve_socp",
 ]
 
 OUTCOME_BYTES = 32  # sizeof(socp_outcome): int32 status, int32 iters, double rd, rp, gap
@@ -125,6 +126,8 @@ def load():
         L.socp_sqr_record_bytes.argtypes = [vp]
         L.socp_sqr_record_bytes.restype = C.c_int64
         L.socp_sqr_destroy.argtypes = [vp]
+        if hasattr(L, "socp_sqr_solve_socp"):
+            L.socp_sqr_solve_socp.argtypes = [vp] + [dp] * 3 + [C.POINTER(Params)] + [dp] * 4 + [i32p, i32p, dp]
     if hasattr(L, "socp_ingest_create"):  # pipelined ingest (absent from older A/B builds)
         L.socp_ingest_create.argtypes = common + [C.c_int32, C.POINTER(C.c_void_p)]
         L.socp_ingest_next_inputs.argtypes = [vp] + [C.POINTER(C.c_void_p)] * 6

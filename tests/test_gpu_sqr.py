@@ -374,3 +374,121 @@ def test_sqr_workgroup_failures_isolated(oracle):
     assert np.isnan(out["cx"][2 * n:3 * n]).all()
     for p in (0, 1, 3, 4):
         assert np.array_equal(out["cx"][p * n:(p + 1) * n], ref["cx"][p * n:(p + 1) * n])
+
+
+# ---------------------------------------------------------------- solve_socp
+# solve_socp(prob, SolverState(prob, SparseSolver(prob))) -- the reference's own
+# tested configuration (runtests.jl:143-144, 188-189) -- batched on the device
+# (socp_sqr_solve_socp).  The oracle's F_SQR mode restates the same algorithm
+# (sqrscalings.jl / spsolver.jl in the solver.jl loop).
+
+@pytest.mark.parametrize("name", ["soc1", "soc2", "soc3"])
+def test_sqr_solve_socp_runtests_kats(kats, oracle, name):
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from problems import kat_problem
+    q = kats[name]
+    cones, c, A, b, G, h = kat_problem(q)
+    prob = S.Problem(c, A, b, G, h, cones)
+    ss = S.SolverState(prob, S.SparseSolver(prob))
+    st = S.solve_socp(prob, ss)
+    assert ss.status == S.CONVERGED
+    assert np.linalg.norm(st.x - np.array(q["x_expect"])) < q["tol"]  # runtests.jl's own assertion
+    r = oracle.solve_trace(cones, c, A, b, G, h, params=oracle.Params(flags=oracle.F_SQR))
+    assert r["status"] == 0
+    assert abs(ss.iters - r["iters"]) <= 1
+    assert np.abs(st.x - r["x"]).max() <= 1e-3
+
+
+@pytest.mark.parametrize("cfg,K", [(C1, 3), (C2, 4), (C2, 6)])
+def test_sqr_solve_socp_trajectory(oracle, cfg, K):
+    """Fixed-K solves (tol = 0) from the same start: the HIP rank-update IPM
+    against the oracle's F_SQR IPM, relative error of x, z, s <= 1e-8 (SURVEY
+    §8(c) P4's gate; the W = I initial solve and the oracle's LU initial solve
+    agree to rounding)."""
+    B = 32
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                           sing=np.zeros(B, np.uint8), params=oracle.Params(maxit=K, tol=0.0, flags=oracle.F_SQR))
+    hd = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, d["A"], d["G"], np.zeros(B, np.uint8))
+    g = hd.solve_socp(d["c"], d["b"], d["h"], maxit=K, tol=0.0)
+    assert S.default_context().last_kernel_name() == "socp_sqr_solve_socp"
+    assert (g["status"] == r["status"]).all()
+    assert (g["iters"] == r["iters"]).all()
+    for p in range(B):
+        for key, L in (("x", cfg.n), ("z", cfg.k), ("s", cfg.k)):
+            a_, b_ = g[key][p * L:(p + 1) * L], r[key][p * L:(p + 1) * L]
+            e = np.linalg.norm(a_ - b_) / np.linalg.norm(b_)
+            assert e <= 1e-8, (p, key, e)
+
+
+def test_sqr_solve_socp_reference_rule_outcomes(oracle):
+    """The reference stopping rule (tol = 1e-5 absolute, maxit = 40) on 256 C2
+    problems: outcome statistics of the HIP rank-update IPM vs the oracle's
+    F_SQR IPM (late iterations are decided at rounding level, SURVEY §0.7, so
+    the gates are statistical, as for the dense path)."""
+    cfg, B = C2, 256
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                           sing=np.zeros(B, np.uint8), params=oracle.Params(flags=oracle.F_SQR))
+    hd = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, d["A"], d["G"], np.zeros(B, np.uint8))
+    g = hd.solve_socp(d["c"], d["b"], d["h"])
+    hg = np.bincount(g["status"], minlength=5)
+    hr = np.bincount(r["status"], minlength=5)
+    print("HIP", hg.tolist(), "oracle", hr.tolist())
+    conv = (g["status"] == 0) & (r["status"] == 0)
+    oc = r["status"] == 0
+    assert hg[0] >= hr[0] - 0.03 * B, (hg, hr)
+    assert conv.sum() >= 0.9 * oc.sum(), (conv.sum(), oc.sum())
+    assert (np.abs(g["iters"][conv] - r["iters"][conv]) <= 1).mean() >= 0.95
+    # converged problems satisfy the exit test at the returned iterate
+    res = g["res"].reshape(B, 3)
+    assert (res[g["status"] == 0].sum(axis=1) < 1e-5).all()
+    dx = np.abs(g["x"].reshape(B, -1) - r["x"].reshape(B, -1)).max(axis=1)
+    assert np.median(dx[conv]) <= 1e-3
+
+
+def test_sqr_solve_socp_optimal_control_n150(oracle):
+    """runtests.jl:204-244, the problem the reference times on SparseSolver:
+    end to end on the workgroup kernels (n = 150, m = 102, sing)."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from problems import optimal_control
+    cones, c, A, b, G, h = optimal_control(50)
+    prob = S.Problem(c, A, b, G, h, cones)
+    assert prob.sing
+    ss = S.SolverState(prob, S.SparseSolver(prob))
+    st = S.solve_socp(prob, ss)
+    r = oracle.solve_trace(cones, c, A, b, G, h, params=oracle.Params(flags=oracle.F_SQR))
+    assert ss.status == r["status"] == 0, (ss.status, r["status"])
+    assert abs(ss.iters - r["iters"]) <= 1
+    assert np.abs(st.x - r["x"]).max() <= 1e-3 * max(1.0, np.abs(r["x"]).max())
+
+
+def test_sqr_solve_socp_isolation_and_device(oracle):
+    """One problem broken (NaN in its h) stops alone -- its neighbours are
+    bit-identical to a clean batch; device tensors give the host results bit
+    for bit."""
+    import torch
+    cfg, B = C1, 16
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    hd = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, d["A"], d["G"], np.zeros(B, np.uint8))
+    clean = hd.solve_socp(d["c"], d["b"], d["h"])
+    hbad = d["h"].copy()
+    hbad[5 * cfg.k + 3] = np.nan
+    bad = hd.solve_socp(d["c"], d["b"], hbad)
+    assert bad["status"][5] != 0
+    for p in range(B):
+        if p == 5:
+            continue
+        assert bad["status"][p] == clean["status"][p] and bad["iters"][p] == clean["iters"][p]
+        assert np.array_equal(bad["x"][p * cfg.n:(p + 1) * cfg.n], clean["x"][p * cfg.n:(p + 1) * cfg.n])
+    dev = {key: torch.from_numpy(np.ascontiguousarray(v)).cuda() for key, v in d.items() if key in "cAbGh"}
+    hdd = S.SqrHandle(cfg.cones, cfg.n, cfg.m, cfg.k, dev["A"], dev["G"],
+                      torch.zeros(B, dtype=torch.uint8, device="cuda"))
+    gd = hdd.solve_socp(dev["c"], dev["b"], dev["h"])
+    torch.cuda.synchronize()
+    for key in ("x", "y", "z", "s", "iters", "status", "res"):
+        assert np.array_equal(gd[key].cpu().numpy(), clean[key]), key

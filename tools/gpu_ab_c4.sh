@@ -4,7 +4,7 @@
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_large.py -q -x -m gpu --timeout 200 --timeout-method thread > gpurun_out/pytest_large.log 2>&1 || { tail -40 gpurun_out/pytest_large.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_large.py -q -x --tb=short -m gpu --timeout 200 --timeout-method thread > gpurun_out/pytest_large.log 2>&1 || { tail -40 gpurun_out/pytest_large.log; exit 1; }
 tail -1 gpurun_out/pytest_large.log
 for rep in 1 2; do
   for v in default "$@"; do
