@@ -269,6 +269,20 @@ def sqr_bench(args, emit=True):
     ms_setup = sum(t_setup) / len(t_setup)
     ms_solve = sum(t_solve) / len(t_solve)
     st = torch.bincount(out["status"].long(), minlength=5).tolist()
+    # the whole IPM on this plugin (socp_sqr_solve_socp, solve_socp with
+    # SparseSolver): initial point + fixed-K iterations, the dense headline's mode
+    Kf = cfg.fixed_k
+    ipm = hd.solve_socp(c, b, h, maxit=Kf, tol=0.0)
+    ctx.sync()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        ipm = hd.solve_socp(c, b, h, maxit=Kf, tol=0.0)
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt_ipm = time.perf_counter() - t1
+    ipm_iters = int(ipm["iters"].sum().item())
+    ipm_st = torch.bincount(ipm["status"].long(), minlength=5).tolist()
     fs, fv, bs, bv = sqr_model(n, m, k, cfg.cones)
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json):
@@ -292,6 +306,10 @@ def sqr_bench(args, emit=True):
                    "global_batch": B, "parallelism": "dp1"},
         "kernels": {"socp_sqr_setup_kernel_ms": ms_setup, "socp_sqr_solve_kernel_ms": ms_solve},
         "status_counts": st,
+        "solve_socp": {"value": ipm_iters * args.steps / dt_ipm, "unit": "problem-iterations/s",
+                       "ms_per_solve": dt_ipm / args.steps * 1e3, "status_counts": ipm_st,
+                       "mode": f"socp_sqr_solve_socp: initial point + fixed-K={Kf} IPM iterations (tol=0) "
+                               "with SqrScaling + the rank-update factor, device tensors"},
         "roofline": {"bound": "hbm", "kernel": f"socp_sqr_{dominant}_kernel", "achieved": ach,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
                      "traffic": traffic if dominant == "setup" else None,
@@ -464,6 +482,7 @@ def main():
                                               traffic_json=None), emit=False)
             line["rank_update_plugin"] = {"value": sq["value"], "unit": sq["unit"], "ms_per_step": sq["ms_per_step"],
                                           "kernels_ms": sq["kernels"], "status_counts": sq["status_counts"],
+                                          "solve_socp": sq["solve_socp"],
                                           "mode": "bench.py --mode sqr (setup_iter + 2 x solve_kkt per problem)"}
         if not args.no_cpu and world == 1:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol)

@@ -80,7 +80,8 @@ def lib():
         L.or_compute_scaling.argtypes = cones + [C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]
         L.or_compute_scaling.restype = C.c_int
         L.or_scale.argtypes = cones + [_dp, _dp, _dp, _dp, C.c_int]
-        L.or_kkt_single.argtypes = cones + [C.c_int] * 3 + [_dp, _dp, C.c_int] + [_dp] * 6 + [_dp] * 4 + [C.c_void_p, C.c_void_p]
+        L.or_kkt_single.argtypes = (cones + [C.c_int] * 3 + [_dp, _dp, C.c_int] + [_dp] * 6 + [_dp] * 4
+                                    + [C.c_void_p, C.c_void_p, C.c_int])
         L.or_kkt_single.restype = C.c_int
         L.or_sqr_kkt_single.argtypes = cones + [C.c_int] * 3 + [_dp, _dp, C.c_int] + [_dp] * 6 + [_dp] * 4 + [C.c_void_p] * 4
         L.or_sqr_kkt_single.restype = C.c_int
@@ -162,8 +163,10 @@ def scale(cones, wbs, mu, x, inverse=False):
     return out
 
 
-def kkt_single(cones, A, G, sing, s, z, dx, dy, dz, ds, want_H=False):
-    """compute_scaling + setup_iter + solve_kkt (densesolver.jl:41-90) at iterate (s,z)."""
+def kkt_single(cones, A, G, sing, s, z, dx, dy, dz, ds, want_H=False, structured=False):
+    """compute_scaling + setup_iter + solve_kkt (densesolver.jl:41-90) at iterate (s,z).
+    structured: the kernels' order (X = W^-1 G per cone, H = X'X; F_STRUCTURED)
+    instead of the reference's (dense iW*iW', G'*iWiW*G); no H output then."""
     A = np.asarray(A, dtype=np.float64).reshape(-1, G.shape[1]) if np.size(A) else np.zeros((0, G.shape[1]))
     m, n = A.shape
     k = G.shape[0]
@@ -173,7 +176,8 @@ def kkt_single(cones, A, G, sing, s, z, dx, dy, dz, ds, want_H=False):
     st = lib().or_kkt_single(*cone_arrays(cones), n, m, k, _f(A.ravel(order="F")) if m else np.zeros(1),
                              _f(G.ravel(order="F")), int(sing), _f(s), _f(z), _f(dx),
                              _f(dy) if m else np.zeros(1), _f(dz), _f(ds), cx, cy if m else np.zeros(1), cz, cs,
-                             H.ctypes.data if want_H else None, Li.ctypes.data if want_H else None)
+                             H.ctypes.data if want_H else None, Li.ctypes.data if want_H else None,
+                             int(bool(structured)))
     out = dict(cx=cx, cy=cy, cz=cz, cs=cs, status=st)
     if want_H:
         out["H"] = H.reshape(n, n, order="F")

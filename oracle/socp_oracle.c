@@ -1172,7 +1172,7 @@ EXPORT int or_kkt_single(int nc, const int32_t* kind, const int32_t* offs, const
                          int n, int m, int k, const double* A, const double* G, int sing,
                          const double* s, const double* z, const double* dx, const double* dy,
                          const double* dz, const double* ds, double* cx, double* cy, double* cz,
-                         double* cs, double* Hout, double* Liout) {
+                         double* cs, double* Hout, double* Liout, int structured) {
   cones_t C = {nc, kind, offs, dim};
   ws_t w;
   if (ws_init(&w, n, m, k, nc, max_dim(&C))) return -1;
@@ -1180,6 +1180,8 @@ EXPORT int or_kkt_single(int nc, const int32_t* kind, const int32_t* offs, const
   w.D.G = G;
   w.D.sing = sing;
   w.D.C = &C;
+  w.D.structured = structured; /* the kernels' order (F_STRUCTURED); H output: reference order only */
+  if (structured) Hout = NULL;
   for (int bq = 0; bq < n; ++bq)
     for (int a = 0; a < n; ++a) {
       double acc = 0.0;
@@ -1187,7 +1189,7 @@ EXPORT int or_kkt_single(int nc, const int32_t* kind, const int32_t* offs, const
       M(w.D.AA, n, a, bq) = acc;
     }
   int dom = 0;
-  compute_scaling(&C, &w.S, s, z, &dom);
+  compute_scaling_x(&C, &w.S, s, z, &dom, structured);
   int st = 0;
   if (dom) {
     st = 4;

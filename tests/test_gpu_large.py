@@ -268,3 +268,57 @@ def test_large_kkt_backward_error(oracle):
     ref_err = backward(o["cx"], o["cy"], o["cz"], o["cs"])
     assert out["status"][0] == 0
     assert backward(out["cx"], out["cy"], out["cz"], out["cs"]) <= max(1e-12, 10 * ref_err), ref_err
+
+
+@pytest.mark.parametrize("K", [4, 5])
+def test_c4_kkt_backward_error_at_bench_iterates(oracle, K):
+    """P6 at C4's late bench iterates (K = 4, 5, kappa_2(H) ~1e7-1e9), where
+    the trajectory gate of test_c4_trajectory_k1_to_k5_fixture loosens to
+    1e-12 kappa: the blocked kernel's KKT solve (setup_iter + solve_kkt through
+    the dense plugin) at the committed oracle iterate has a backward error
+    within max(1e-12, 10 x) the oracle's own on the same system, in the
+    reference's op order and in the kernels' (structured) order."""
+    import base64
+    import json
+    import os
+    cfg = C4
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "trajectories.json")) as f:
+        cases = [c for c in json.load(f)["cases"] if c["name"].startswith("C4#")][:2]
+    B = len(cases)
+    c, A, b, G, h = (t.cpu().numpy() for t in S.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cases[0]["source"]["seed"]))
+    arr = lambda s: np.frombuffer(base64.b64decode(s), dtype="<f8")  # noqa: E731
+    n, m, k = cfg.n, cfg.m, cfg.k
+    s = np.concatenate([arr(case["iterates"][K]["s"]) for case in cases])
+    z = np.concatenate([arr(case["iterates"][K]["z"]) for case in cases])
+    hd = S.DenseHandle(cfg.cones, n, m, k, A, G, np.zeros(B, np.uint8))
+    assert (hd.setup_iter(s, z) == 0).all()
+    rng = np.random.default_rng(40 + K)
+    rhs = [rng.standard_normal(B * q) for q in (n, m, k, k)]
+    got = hd.solve_kkt(*rhs)
+    for p in range(B):
+        sl = lambda v, q: v[p * q:(p + 1) * q]  # noqa: E731
+        pA = A[p * m * n:(p + 1) * m * n].reshape(n, m).T
+        pG = G[p * k * n:(p + 1) * k * n].reshape(n, k).T
+        r = [sl(rhs[0], n), sl(rhs[1], m), sl(rhs[2], k), sl(rhs[3], k)]
+        ps, pz = sl(s, k), sl(z, k)
+        sc = oracle.compute_scaling(cfg.cones, ps, pz)
+        W, lam = sc["W"], sc["l"]
+
+        def backward(cx, cy, cz, cs):
+            r1 = pA.T @ cy + pG.T @ cz - r[0]
+            r2 = pA @ cx - r[1]
+            r3 = pG @ cx + cs - r[2]
+            r4 = oracle.vprod(cfg.cones, lam, W @ cz + np.linalg.solve(W.T, cs)) - r[3]
+            scale = max(np.abs(np.concatenate(r)).max(), np.abs(np.concatenate([cx, cy, cz, cs])).max())
+            return max(np.abs(q).max() for q in (r1, r2, r3, r4)) / scale
+
+        o = oracle.kkt_single(cfg.cones, pA, pG, False, ps, pz, *r)
+        ref = backward(o["cx"], o["cy"], o["cz"], o["cs"])
+        q = oracle.kkt_single(cfg.cones, pA, pG, False, ps, pz, *r, structured=True)
+        ref_s = backward(q["cx"], q["cy"], q["cz"], q["cs"])
+        mine = backward(sl(got["cx"], n), sl(got["cy"], m), sl(got["cz"], k), sl(got["cs"], k))
+        print(f"K={K} p={p}: backward error {mine:.2e}, oracle reference order {ref:.2e}, structured {ref_s:.2e}")
+        # against the reference op order (which loses all accuracy by K = 5 here)
+        # and against the same algorithm in the oracle (the meaningful bound)
+        assert mine <= max(1e-12, 10 * ref), (K, p, mine, ref)
+        assert mine <= max(1e-12, 10 * ref_s), (K, p, mine, ref_s)
