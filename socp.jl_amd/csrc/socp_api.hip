@@ -1319,10 +1319,10 @@ extern "C" int socp_generate(socp_ctx* ctx, const socp_dims* dims, const int32_t
 // nonzeros (column by column: the column of nonzero e is found by a binary
 // search of colptr, so the scatter is one pass over nz).  A first pass checks
 // that every column's row indices are strictly increasing; a problem where one
-// is not (duplicates, or unsorted indices as a hand-built CSC may have) sums
-// every entry with atomics instead of storing it, so repeated (i, j) entries
-// add up, as sparse() does.  Sums of three or more duplicates may then round
-// in either order.
+// is not (duplicates, or unsorted indices as a hand-built CSC may have) is
+// packed a thread per column instead, each column's entries summed in input
+// order, so repeated (i, j) entries add up as sparse() does and the result is
+// deterministic bit for bit.
 namespace {
 __device__ __forceinline__ int csc_col(const int64_t* cp, int cols, int64_t base, int64_t e) {
   int lo = 0, hi = cols;  // invariant: cp[lo] - base <= e < cp[hi] - base
@@ -1354,18 +1354,29 @@ __global__ void __launch_bounds__(256) socp_pack_csc_kernel(int32_t rows, int32_
     if (e + 1 < cp[j + 1] - base && rowval[n0 + e + 1] <= rowval[n0 + e]) unsorted = 1;
   }
   __syncthreads();
-  const bool add = unsorted != 0;
-  for (int64_t e = threadIdx.x; e < nnz; e += blockDim.x) {
-    const int j = csc_col(cp, cols, base, e);
-    const int64_t i = rowval[n0 + e] - base;
-    if (i < 0 || i >= rows) {
-      atomicOr(err, 2);
-      continue;
-    }
-    if (add)
-      atomicAdd(D + (int64_t)j * rows + i, nzval[n0 + e]);
-    else
+  if (unsorted == 0) {  // canonical CSC (SparseMatrixCSC): one store per nonzero
+    for (int64_t e = threadIdx.x; e < nnz; e += blockDim.x) {
+      const int j = csc_col(cp, cols, base, e);
+      const int64_t i = rowval[n0 + e] - base;
+      if (i < 0 || i >= rows) {
+        atomicOr(err, 2);
+        continue;
+      }
       D[(int64_t)j * rows + i] = nzval[n0 + e];
+    }
+    return;
+  }
+  // unsorted or duplicate row indices: a thread per column sums its entries in
+  // input order (sparse()'s combine), so the result is deterministic bit for bit
+  for (int j = threadIdx.x; j < cols; j += blockDim.x) {
+    for (int64_t e = cp[j] - base; e < cp[j + 1] - base; ++e) {
+      const int64_t i = rowval[n0 + e] - base;
+      if (i < 0 || i >= rows) {
+        atomicOr(err, 2);
+        continue;
+      }
+      D[(int64_t)j * rows + i] += nzval[n0 + e];
+    }
   }
 }
 }  // namespace

@@ -416,6 +416,28 @@ def test_pack_csc_unsorted_nonadjacent_duplicates():
     assert got[3, 0] == 5.0 and got[5, 0] == 2.0 and np.count_nonzero(got) == 2
 
 
+def test_pack_csc_duplicates_sum_in_input_order():
+    """three or more duplicates of one (i, j) are summed in
+    input order (a thread per column), so the packed value is the sequential
+    sum bit for bit -- values chosen so that the order changes the rounding."""
+    import torch
+    rows, cols, B = 4, 2, 64
+    dev = torch.device("cuda", 0)
+    i64 = dict(dtype=torch.int64, device=dev)
+    vals = [1.0, 1e-16, 1e-16, -1.0, 3e-16, 0.5]  # all into (2, 0), then (1, 1)
+    colptr = torch.tensor([0, 5, 6] * B, **i64)
+    rowval = torch.tensor(([2, 2, 2, 2, 2, 1]) * B, **i64)
+    nzval = torch.tensor(vals * B, dtype=torch.float64, device=dev)
+    nz_offs = torch.arange(0, 6 * B + 1, 6, **i64)
+    seq = 0.0
+    for v in vals[:5]:
+        seq += v
+    for _ in range(3):
+        got = S.pack_csc((nz_offs, colptr, rowval, nzval), rows, cols, index_base=0).cpu().numpy().reshape(B, cols, rows)
+        assert (got[:, 0, 2] == seq).all() and (got[:, 1, 1] == 0.5).all()
+        assert np.count_nonzero(got) == 2 * B
+
+
 def test_batch_above_int32_rejected():
     """the persistent kernels index problems with an int32 counter."""
     import ctypes as C
