@@ -278,6 +278,48 @@ function solve_socp_batched(problems::AbstractVector{<:Problem}; maxit=40, tol=1
     return states, iters, status
 end
 
+"""
+    solve_socp_batched_sqr(problems; maxit=40, tol=1e-5) -> (states, iters, status)
+
+The same batch through the rank-update plugin: `solve_socp(prob,
+SolverState(prob, SparseSolver(prob)))` for every problem, the reference's own
+tested configuration, as one device solve (`socp_sqr_create` +
+`socp_sqr_solve_socp`; failures per problem, no throw).
+"""
+function solve_socp_batched_sqr(problems::AbstractVector{<:Problem}; maxit=40, tol=1e-5)
+    p0 = problems[1]
+    n, m, k = p0.n, p0.m, p0.k
+    B = length(problems)
+    kind, offs, dim = cone_arrays(p0.cones)
+    c = reduce(vcat, [p.c for p in problems])
+    A = reduce(vcat, [vec(Matrix(p.A)) for p in problems])
+    b = reduce(vcat, [p.b for p in problems])
+    G = reduce(vcat, [vec(Matrix(p.G)) for p in problems])
+    h = reduce(vcat, [p.h for p in problems])
+    sing = UInt8[typeof(p).parameters[5] ? 1 : 0 for p in problems]
+    dims = Ref(SocpDims(B, n, m, k, length(p0.cones)))
+    hd = Ref{Ptr{Cvoid}}(C_NULL)
+    socp_check(ccall((:socp_sqr_create, libsocp), Cint,
+                     (Ptr{Cvoid}, Ref{SocpDims}, Ptr{Int32}, Ptr{Int32}, Ptr{Int32},
+                      Ptr{Float64}, Ptr{Float64}, Ptr{UInt8}, Int32, Ptr{Ptr{Cvoid}}),
+                     socp_ctx(), dims, kind, offs, dim, A, G, sing, Int32(0), hd))
+    x, y, z, s = zeros(B * n), zeros(B * m), zeros(B * k), zeros(B * k)
+    iters, status = zeros(Int32, B), zeros(Int32, B)
+    params = Ref(SocpParams(maxit, 3, tol, 0.99, 1e-10, 0, 0))
+    try
+        socp_check(ccall((:socp_sqr_solve_socp, libsocp), Cint,
+                         (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{SocpParams},
+                          Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32},
+                          Ptr{Float64}),
+                         hd[], c, b, h, params, x, y, z, s, iters, status, C_NULL))
+    finally
+        ccall((:socp_sqr_destroy, libsocp), Cint, (Ptr{Cvoid},), hd[])
+    end
+    states = [State(problems[i], x[(i-1)*n+1:i*n], y[(i-1)*m+1:i*m], z[(i-1)*k+1:i*k], s[(i-1)*k+1:i*k])
+              for i in 1:B]
+    return states, iters, status
+end
+
 # ------------------------------------------------------- multi-GPU gather
 # One process per GPU (e.g. under MPI.jl); problems shard by contiguous global
 # index and the only collective is the RCCL all-gather of each problem's
