@@ -45,7 +45,7 @@ __host__ __device__ inline LargeLayout large_layout(int n, int m, int k) {
   L.o_kv = o;   o += 15 * L.KP;     // k-vectors
   L.o_nv = o;   o += 6 * L.NPAD;    // n-vectors
   L.o_mv = o;   o += 5 * L.MPAD;    // m-vectors
-  L.o_row = o;  o += 2 * L.RW;      // sweep pivot-row buffers
+  L.o_row = o;  o += 2 * L.RW > 1024 ? 2 * L.RW : 1024;  // sweep: pivot rows / four 16x16 tile slots
   L.o_rv = o;   o += 64;            // sweep: -1/d of the panel's pivots
   L.o_part = o; o += 8 * L.MPAD;    // A x partial sums per wavefront
   L.o_red = o;  o += 64;            // block reductions

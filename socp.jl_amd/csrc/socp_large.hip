@@ -24,6 +24,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#define SOCP_MULTI_WAVE 1  // LANE_IDS / factor_tile: lanes of 8-wavefront workgroups
 #include "socp_kernels.hpp"
 
 namespace socp {
@@ -87,6 +88,19 @@ __device__ __forceinline__ double wave_max(double v) {
   double x[1] = {v};
   dpp_scan<1>(x, (int)(threadIdx.x & 63), 0, true);
   return readlane_d(x[0], 63);
+}
+
+#ifndef SOCP_LG_PANEL
+#define SOCP_LG_PANEL 1  // 0: the per-pivot rank-1 sweep of a panel (A/B builds)
+#endif
+
+// C += U'V (NEG = 1: C -= U'V) for C/D-layout 16x16 tiles (socp_small.hpp's
+// tile algebra: lane (g, cl) holds X[g+4r][cl] in register r)
+template <int NEG>
+__device__ __forceinline__ d4 tile_mm(const d4& U, const d4& V, d4 C) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) C = __builtin_amdgcn_mfma_f64_16x16x4f64(U[s], V[s], C, 0, 0, NEG);
+  return C;
 }
 
 struct Large {
@@ -885,6 +899,170 @@ struct Large {
     BAR();
   }
 
+  // One panel of the sweep below by 16x16 tiles on MFMA: the 64 rank-1 pivot
+  // steps regrouped into a tile Cholesky of the pivot block.  With D = M_PP =
+  // L L' (tile rows t = 0..3 of the panel; W_t = L_tt^-1 by factor_tile, whose
+  // 4x4 pivots are D's Cholesky pivots: the same potrf failure test):
+  //   forward  Y_t = W_t (R_t - sum_{s<t} L_ts Y_s), L_ts = Y(s, P-tile t)'
+  //            -- Y = L^-1 M_P, the rows the Gram updates read (fv = -1);
+  //            in the P block Y = L', whose lower tiles are replaced by
+  //            E = L^-1 (the identity's forward pass);
+  //   backward Z_t = W_t' (Y_t - sum_{u>t} L_ut' Z_u)
+  //            -- Z = D^-1 M_P off the P block, D^-1 = L'^-1 E in it;
+  //   M_P <- Z, M_PP <- -D^-1 (its lower triangle, from one tile of each
+  //   mirrored pair: every element has one writer).
+  // Wave w holds tile columns j = w + 8i of the panel's four tile rows; each
+  // of the 4 + 4 steps publishes the tiles the others need through four LDS
+  // tile slots at o_row (8 LDS barriers per panel instead of 64 pivot steps).
+  template <int nb>
+  __device__ __forceinline__ bool panel_tiles(gdbl* M, int ld, int P) {
+    constexpr int NT = 4 * nb, NJ = (NT + NW - 1) / NW;
+    const int w = wv, RW = L.RW, P0 = 64 * P, ob = L.o_row, of = L.o_rv;
+    gdbl* const Y = Yp + (int64_t)P * 64 * RW;
+    const d4 zero = {0.0, 0.0, 0.0, 0.0};
+    d4 R[4][NJ];
+    {
+      LANE_IDS();
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {
+        const int j = w + NW * i;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int x = P0 + 16 * t + g + 4 * r, y = 16 * j + cl;  // element (x, y), lower triangle
+            R[t][i][r] = j < NT ? M[(y <= x) ? (int64_t)y * ld + x : (int64_t)x * ld + y] : 0.0;
+          }
+      }
+    }
+    // ---- forward pass
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      LANE_IDS();
+      const int jd = 4 * P + t, od = jd % NW, id = jd / NW;
+      if (w == od) {
+        d4 C = zero, Ys[4];
+#pragma unroll
+        for (int i = 0; i < NJ; ++i)
+          if (i == id) {
+            C = R[t][i];
+#pragma unroll
+            for (int s_ = 0; s_ < t; ++s_) Ys[s_] = R[s_][i];
+          }
+#pragma unroll
+        for (int s_ = 0; s_ < t; ++s_) C = tile_mm<1>(Ys[s_], Ys[s_], C);  // D_tt - sum L_ts L_ts'
+        d4 Wt;
+        bool ok = true;
+        factor_tile(C, Wt, ok);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int s_ = 0; s_ < t; ++s_) LV(ob + 256 * s_ + 64 * r + lane) = Ys[s_][r];
+          LV(ob + 768 + 64 * r + lane) = Wt[r];
+        }
+        if (lane == 0) LV(of + t) = ok ? 0.0 : 1.0;
+#pragma unroll
+        for (int i = 0; i < NJ; ++i)
+          if (i == id) R[t][i] = Wt;  // E's diagonal tile
+      }
+      LDS_BAR();
+      d4 Yb[4], WT;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int s_ = 0; s_ < t; ++s_) Yb[s_][r] = LV(ob + 256 * s_ + 64 * r + lane);
+        WT[r] = LV(ob + 768 + 64 * (cl >> 2) + 16 * (cl & 3) + g + 4 * r);  // W_t'
+      }
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {
+        const int j = w + NW * i;
+        if (j >= NT || j == jd) continue;
+        const int u = ((j >> 2) == P) ? (j & 3) : -1;  // P-block tile column index
+        d4 X = (u >= 0 && u < t) ? zero : R[t][i];      // E: the identity's zero below
+#pragma unroll
+        for (int s_ = 0; s_ < t; ++s_)
+          if (u < 0 || u >= t || s_ >= u) X = tile_mm<1>(Yb[s_], R[s_][i], X);
+        R[t][i] = tile_mm<0>(WT, X, zero);
+      }
+      LDS_BAR();
+    }
+    bool ok = true;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) ok = ok && LV(of + t) == 0.0;
+    if (!ok) return false;  // uniform: every wave read the same flags
+    {
+      // the Gram updates' rows: Y off the P block, and fv = -1 (rows are L^-1-scaled)
+      LANE_IDS();
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {
+        const int j = w + NW * i;
+        if (j >= NT || (j >> 2) == P) continue;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Y[(int64_t)(16 * t + g + 4 * r) * RW + 16 * j + cl] = R[t][i][r];
+      }
+      if (tid < 64) Rv[P0 + tid] = -1.0;
+    }
+    // ---- backward pass
+#pragma unroll
+    for (int t = 3; t >= 0; --t) {
+      LANE_IDS();
+#pragma unroll
+      for (int u = t; u < 4; ++u) {
+        const int jj = 4 * P + u;
+        if (w == jj % NW) {
+#pragma unroll
+          for (int i = 0; i < NJ; ++i)
+            if (i == jj / NW) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) LV(ob + 256 * u + 64 * r + lane) = R[t][i][r];  // W_t, Y(t, P-tile u)
+            }
+        }
+      }
+      LDS_BAR();
+      d4 Wt, YT[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Wt[r] = LV(ob + 256 * t + 64 * r + lane);
+#pragma unroll
+        for (int u = t + 1; u < 4; ++u) YT[u][r] = LV(ob + 256 * u + 64 * (cl >> 2) + 16 * (cl & 3) + g + 4 * r);
+      }
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {
+        const int j = w + NW * i;
+        if (j >= NT) continue;
+        const int v = ((j >> 2) == P) ? (j & 3) : -1;
+        d4 X = (v > t) ? zero : R[t][i];  // in the P block: E (zero above its diagonal)
+#pragma unroll
+        for (int u = t + 1; u < 4; ++u) X = tile_mm<1>(YT[u], R[u][i], X);
+        R[t][i] = tile_mm<0>(Wt, X, zero);
+      }
+      LDS_BAR();
+    }
+    {
+      LANE_IDS();
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {
+        const int j = w + NW * i;
+        if (j >= NT) continue;
+        const bool pb = (j >> 2) == P;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int x = P0 + 16 * t + g + 4 * r, y = 16 * j + cl;
+            if (pb) {
+              if (y <= x) M[(int64_t)y * ld + x] = -R[t][i][r];
+            } else {
+              M[(y <= x) ? (int64_t)y * ld + x : (int64_t)x * ld + y] = R[t][i][r];
+            }
+          }
+      }
+    }
+    return true;
+  }
+
   // Blocked symmetric Gauss-Jordan sweep of the 64nb x 64nb symmetric matrix
   // whose lower triangle is stored in M (column-major, ld); leaves -M^-1 in the
   // lower triangle.  Panel P: thread (wave w, lane l) holds panel rows
@@ -926,6 +1104,11 @@ struct Large {
       }
       BAR();
       LSTAMP(NSTAMP + 1 + 0);
+#if SOCP_LG_PANEL
+      const bool ok = panel_tiles<nb>(M, ld, P);
+      LSTAMP(NSTAMP + 1 + 1);
+      if (!ok) return false;
+#else
       double Z[8][nb];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -1000,7 +1183,7 @@ struct Large {
       {
         // addresses recomputed from a fresh lane id: reusing the load's would
         // keep 64 of them live (spilled) across the step loop
-        const int lf = lane_fresh() & 63;
+        const int lf = lane_fresh();
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int x = P0 + rr + 8 * q;
@@ -1011,6 +1194,7 @@ struct Large {
           }
         }
       }
+#endif
       BAR();  // panel P written back before the next catch-up reads its neighbours
       LSTAMP(NSTAMP + 1 + 2);
     }

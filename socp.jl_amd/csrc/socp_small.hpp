@@ -260,8 +260,11 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // Lane ids re-read inside each phase (LANE_IDS shadows the members): values
 // derived from them (4*pp + g, 16*ti + cl, ...) are then recomputed where they
 // are used instead of being hoisted out of the persistent loop and kept live.
+#ifndef SOCP_MULTI_WAVE
+#define SOCP_MULTI_WAVE 0  // 1: workgroups of several wavefronts (socp_large.hip defines it)
+#endif
 __device__ __forceinline__ int lane_fresh() {
-  int v = (int)threadIdx.x;
+  int v = SOCP_MULTI_WAVE ? (int)threadIdx.x & 63 : (int)threadIdx.x;  // the lane in its wavefront
   asm volatile("" : "+v"(v));
   return v;
 }
@@ -425,6 +428,160 @@ enum : int {
   MP_SOLVE_HEAD, MP_SOLVE_MAT, MP_SOLVE_TAIL, MP_SAVE
 };
 enum : int { RET_INIT, RET_KKT, RET_AFFINE, RET_COMBINED };
+
+// ---------------------------------------- 16x16 tile kernels (shared by the
+// register kernel's H^-1 sweep and the blocked kernel's panel factorisation)
+
+// Broadcast across the four 16-lane rows: every lane gets x from the lane of
+// row R with the same column index (gfx950 v_permlane32_swap / 16_swap).
+template <int R>
+__device__ __forceinline__ double row_bcast(double x) {
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto a32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const unsigned ylo = (R < 2) ? a32[0] : a32[1], yhi = (R < 2) ? b32[0] : b32[1];
+  const auto a16 = __builtin_amdgcn_permlane16_swap(ylo, ylo, false, false);
+  const auto b16 = __builtin_amdgcn_permlane16_swap(yhi, yhi, false, false);
+  const unsigned zlo = (R & 1) ? a16[1] : a16[0], zhi = (R & 1) ? b16[1] : b16[0];
+  return __hiloint2double((int)zhi, (int)zlo);
+}
+
+// All four row broadcasts of x at once: out[R] = x of row R, same column index.
+__device__ __forceinline__ void row_bcast4(double x, double (&out)[4]) {
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto a32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto a16 = __builtin_amdgcn_permlane16_swap(a32[h], a32[h], false, false);
+    const auto b16 = __builtin_amdgcn_permlane16_swap(b32[h], b32[h], false, false);
+    out[2 * h] = __hiloint2double((int)b16[0], (int)a16[0]);
+    out[2 * h + 1] = __hiloint2double((int)b16[1], (int)a16[1]);
+  }
+}
+
+// x^-1/2: v_rsq_f64 + two Newton steps (within 1 ulp)
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double y = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * d;
+  double e = fma(-(h * y), y, 0.5);
+  y = fma(y, e, y);
+  e = fma(-(h * y), y, 0.5);
+  return fma(y, e, y);
+}
+
+#ifndef SOCP_TILE_FACTOR
+#define SOCP_TILE_FACTOR 1
+#endif
+#ifndef SOCP_TRANSPOSE_MFMA
+#define SOCP_TRANSPOSE_MFMA 0
+#endif
+#if SOCP_TILE_FACTOR == 0
+// Pivot J of row block B of the tile factorisation: v = register B of the
+// (updated) D tile, w = register B of the eliminated identity.  Row J of
+// the block (lanes of row group J) is scaled by 1/sqrt(d) and becomes row
+// 4B+J of L' (R) and of W; the rows below it in the block take the rank-1
+// update.  Rows above it (finished) take garbage, never read again.
+template <int B, int J>
+__device__ __forceinline__ void tile_pivot(double& v, double& w, double& R, double& Wb, bool& ok) {
+  if constexpr (J < 4) {
+    LANE_IDS();
+    const double d = readlane_d(v, 16 * J + 4 * B + J);
+    ok = ok && (d > 0.0);  // NaN fails too: potrf's test
+    const double rs = rsqrt_nr(d);
+    const double vj = row_bcast<J>(v) * rs;
+    const double wj = row_bcast<J>(w) * rs;
+    const double l = dpp_all<0x150 + 4 * B + J>(v) * rs;  // D[4B+g][4B+J] / sqrt(d)
+    v = fma(-l, vj, v);
+    w = fma(-l, wj, w);
+    R = (g == J) ? vj : R;
+    Wb = (g == J) ? wj : Wb;
+    tile_pivot<B, J + 1>(v, w, R, Wb, ok);
+  }
+}
+#endif
+// Row blocks B.. of W = L^-1 for D = L L' (right-looking, 4 rows at a time;
+// the rank-4 trailing update of the D and identity tiles is one MFMA each).
+// The 4x4 diagonal block is factored in wave-uniform values (its upper
+// triangle, as potrf('U') reads it), then every lane forms the block's rows
+// of R = L' and of W by forward substitution from the broadcast block rows.
+struct NoHook {
+  template <int B>
+  __device__ __forceinline__ void run() const {}
+};
+template <int B, class H = NoHook>
+__device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok, const H& hook = H()) {
+  if constexpr (B < 4) {
+    LANE_IDS();
+    double R, Wb;
+#if SOCP_TILE_FACTOR == 0
+    {
+      double v = Dt[B], w = It[B];
+      R = 0.0;
+      Wb = 0.0;
+      tile_pivot<B, 0>(v, w, R, Wb, ok);
+    }
+#else
+    {
+      const double v = Dt[B], w = It[B];
+      // a_ij = D[4B+i][4B+j] (i <= j): lane (i, 4B+j) of register B
+      const double a00 = readlane_d(v, 4 * B), a01 = readlane_d(v, 4 * B + 1),
+                   a02 = readlane_d(v, 4 * B + 2), a03 = readlane_d(v, 4 * B + 3);
+      const double a11 = readlane_d(v, 16 + 4 * B + 1), a12 = readlane_d(v, 16 + 4 * B + 2),
+                   a13 = readlane_d(v, 16 + 4 * B + 3);
+      const double a22 = readlane_d(v, 32 + 4 * B + 2), a23 = readlane_d(v, 32 + 4 * B + 3);
+      const double a33 = readlane_d(v, 48 + 4 * B + 3);
+      const double rs0 = rsqrt_nr(a00);
+      const double r01 = a01 * rs0, r02 = a02 * rs0, r03 = a03 * rs0;
+      const double s11 = fma(-r01, r01, a11);
+      const double rs1 = rsqrt_nr(s11);
+      const double r12 = fma(-r01, r02, a12) * rs1, r13 = fma(-r01, r03, a13) * rs1;
+      const double s22 = fma(-r12, r12, fma(-r02, r02, a22));
+      const double rs2 = rsqrt_nr(s22);
+      const double r23 = fma(-r12, r13, fma(-r02, r03, a23)) * rs2;
+      const double s33 = fma(-r23, r23, fma(-r13, r13, fma(-r03, r03, a33)));
+      const double rs3 = rsqrt_nr(s33);
+      ok = ok && (a00 > 0.0) && (s11 > 0.0) && (s22 > 0.0) && (s33 > 0.0);  // NaN fails too
+      double V[4], X[4];
+      row_bcast4(v, V);
+      row_bcast4(w, X);
+      const double R0 = V[0] * rs0;
+      const double R1 = fma(-r01, R0, V[1]) * rs1;
+      const double R2 = fma(-r12, R1, fma(-r02, R0, V[2])) * rs2;
+      const double R3 = fma(-r23, R2, fma(-r13, R1, fma(-r03, R0, V[3]))) * rs3;
+      const double W0 = X[0] * rs0;
+      const double W1 = fma(-r01, W0, X[1]) * rs1;
+      const double W2 = fma(-r12, W1, fma(-r02, W0, X[2])) * rs2;
+      const double W3 = fma(-r23, W2, fma(-r13, W1, fma(-r03, W0, X[3]))) * rs3;
+      R = g == 0 ? R0 : (g == 1 ? R1 : (g == 2 ? R2 : R3));
+      Wb = g == 0 ? W0 : (g == 1 ? W1 : (g == 2 ? W2 : W3));
+    }
+#endif
+    hook.template run<B>();  // independent MFMA work interleaved with the chain
+    W[B] = Wb;
+    if constexpr (B < 3) {
+      const d4 t = __builtin_amdgcn_mfma_f64_16x16x4f64(R, R, Dt, 0, 0, 1);   // Dt -= R'R
+      const d4 u = __builtin_amdgcn_mfma_f64_16x16x4f64(R, Wb, It, 0, 0, 1);  // It -= R'W
+#pragma unroll
+      for (int r = B + 1; r < 4; ++r) {
+        Dt[r] = t[r];
+        It[r] = u[r];
+      }
+    }
+    tile_block<B + 1>(Dt, It, W, ok, hook);
+  }
+}
+template <class H = NoHook>
+__device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok, const H& hook = H()) {
+  MARK_BEGIN("factor_tile");
+  LANE_IDS();
+  d4 It;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) It[r] = (g + 4 * r == cl) ? 1.0 : 0.0;
+  W = It;
+  tile_block<0>(Dt, It, W, ok, hook);
+}
+
 
 template <int NQ, int NP, int MQ>
 struct Small {
@@ -1231,34 +1388,6 @@ struct Small {
       }
   }
 
-  // Broadcast across the four 16-lane rows: every lane gets x from the lane of
-  // row R with the same column index (gfx950 v_permlane32_swap / 16_swap).
-  template <int R>
-  __device__ __forceinline__ static double row_bcast(double x) {
-    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-    const auto a32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto b32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-    const unsigned ylo = (R < 2) ? a32[0] : a32[1], yhi = (R < 2) ? b32[0] : b32[1];
-    const auto a16 = __builtin_amdgcn_permlane16_swap(ylo, ylo, false, false);
-    const auto b16 = __builtin_amdgcn_permlane16_swap(yhi, yhi, false, false);
-    const unsigned zlo = (R & 1) ? a16[1] : a16[0], zhi = (R & 1) ? b16[1] : b16[0];
-    return __hiloint2double((int)zhi, (int)zlo);
-  }
-
-  // All four row broadcasts of x at once: out[R] = x of row R, same column index.
-  __device__ __forceinline__ static void row_bcast4(double x, double (&out)[4]) {
-    const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
-    const auto a32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-    const auto b32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const auto a16 = __builtin_amdgcn_permlane16_swap(a32[h], a32[h], false, false);
-      const auto b16 = __builtin_amdgcn_permlane16_swap(b32[h], b32[h], false, false);
-      out[2 * h] = __hiloint2double((int)b16[0], (int)a16[0]);
-      out[2 * h + 1] = __hiloint2double((int)b16[1], (int)a16[1]);
-    }
-  }
-
   // ------------------------------------------------- H^-1 by a block sweep
   // The inverse Li = H^-1 of densesolver.jl:47-48 (cholesky! + potrs(I)) is
   // formed by a symmetric Gauss-Jordan sweep with 16x16 pivot tiles P; after
@@ -1274,16 +1403,6 @@ struct Small {
   // r, so register s of a tile is the k-step-s operand of mfma_f64_16x16x4,
   // and sum_s mfma(U[s], V[s]) = U'V for any two tiles U, V.
 
-  // x^-1/2: v_rsq_f64 + two Newton steps (within 1 ulp)
-  __device__ __forceinline__ static double rsqrt_nr(double d) {
-    double y = __builtin_amdgcn_rsq(d);
-    const double h = 0.5 * d;
-    double e = fma(-(h * y), y, 0.5);
-    y = fma(y, e, y);
-    e = fma(-(h * y), y, 0.5);
-    return fma(y, e, y);
-  }
-
   // sum_s mfma(U[s], V[s], C) with the NEG modifiers of gfx950 f64 MFMA
   // (blgp bit 0 negates A, bit 2 negates C)
   template <int NEG>
@@ -1291,118 +1410,6 @@ struct Small {
 #pragma unroll
     for (int s = 0; s < 4; ++s) C = __builtin_amdgcn_mfma_f64_16x16x4f64(U[s], V[s], C, 0, 0, NEG);
     return C;
-  }
-
-#ifndef SOCP_TILE_FACTOR
-#define SOCP_TILE_FACTOR 1
-#endif
-#ifndef SOCP_TRANSPOSE_MFMA
-#define SOCP_TRANSPOSE_MFMA 0
-#endif
-#if SOCP_TILE_FACTOR == 0
-  // Pivot J of row block B of the tile factorisation: v = register B of the
-  // (updated) D tile, w = register B of the eliminated identity.  Row J of
-  // the block (lanes of row group J) is scaled by 1/sqrt(d) and becomes row
-  // 4B+J of L' (R) and of W; the rows below it in the block take the rank-1
-  // update.  Rows above it (finished) take garbage, never read again.
-  template <int B, int J>
-  __device__ __forceinline__ void tile_pivot(double& v, double& w, double& R, double& Wb, bool& ok) const {
-    if constexpr (J < 4) {
-      LANE_IDS();
-      const double d = readlane_d(v, 16 * J + 4 * B + J);
-      ok = ok && (d > 0.0);  // NaN fails too: potrf's test
-      const double rs = rsqrt_nr(d);
-      const double vj = row_bcast<J>(v) * rs;
-      const double wj = row_bcast<J>(w) * rs;
-      const double l = dpp_all<0x150 + 4 * B + J>(v) * rs;  // D[4B+g][4B+J] / sqrt(d)
-      v = fma(-l, vj, v);
-      w = fma(-l, wj, w);
-      R = (g == J) ? vj : R;
-      Wb = (g == J) ? wj : Wb;
-      tile_pivot<B, J + 1>(v, w, R, Wb, ok);
-    }
-  }
-#endif
-  // Row blocks B.. of W = L^-1 for D = L L' (right-looking, 4 rows at a time;
-  // the rank-4 trailing update of the D and identity tiles is one MFMA each).
-  // The 4x4 diagonal block is factored in wave-uniform values (its upper
-  // triangle, as potrf('U') reads it), then every lane forms the block's rows
-  // of R = L' and of W by forward substitution from the broadcast block rows.
-  struct NoHook {
-    template <int B>
-    __device__ __forceinline__ void run() const {}
-  };
-  template <int B, class H = NoHook>
-  __device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok, const H& hook = H()) const {
-    if constexpr (B < 4) {
-      LANE_IDS();
-      double R, Wb;
-#if SOCP_TILE_FACTOR == 0
-      {
-        double v = Dt[B], w = It[B];
-        R = 0.0;
-        Wb = 0.0;
-        tile_pivot<B, 0>(v, w, R, Wb, ok);
-      }
-#else
-      {
-        const double v = Dt[B], w = It[B];
-        // a_ij = D[4B+i][4B+j] (i <= j): lane (i, 4B+j) of register B
-        const double a00 = readlane_d(v, 4 * B), a01 = readlane_d(v, 4 * B + 1),
-                     a02 = readlane_d(v, 4 * B + 2), a03 = readlane_d(v, 4 * B + 3);
-        const double a11 = readlane_d(v, 16 + 4 * B + 1), a12 = readlane_d(v, 16 + 4 * B + 2),
-                     a13 = readlane_d(v, 16 + 4 * B + 3);
-        const double a22 = readlane_d(v, 32 + 4 * B + 2), a23 = readlane_d(v, 32 + 4 * B + 3);
-        const double a33 = readlane_d(v, 48 + 4 * B + 3);
-        const double rs0 = rsqrt_nr(a00);
-        const double r01 = a01 * rs0, r02 = a02 * rs0, r03 = a03 * rs0;
-        const double s11 = fma(-r01, r01, a11);
-        const double rs1 = rsqrt_nr(s11);
-        const double r12 = fma(-r01, r02, a12) * rs1, r13 = fma(-r01, r03, a13) * rs1;
-        const double s22 = fma(-r12, r12, fma(-r02, r02, a22));
-        const double rs2 = rsqrt_nr(s22);
-        const double r23 = fma(-r12, r13, fma(-r02, r03, a23)) * rs2;
-        const double s33 = fma(-r23, r23, fma(-r13, r13, fma(-r03, r03, a33)));
-        const double rs3 = rsqrt_nr(s33);
-        ok = ok && (a00 > 0.0) && (s11 > 0.0) && (s22 > 0.0) && (s33 > 0.0);  // NaN fails too
-        double V[4], X[4];
-        row_bcast4(v, V);
-        row_bcast4(w, X);
-        const double R0 = V[0] * rs0;
-        const double R1 = fma(-r01, R0, V[1]) * rs1;
-        const double R2 = fma(-r12, R1, fma(-r02, R0, V[2])) * rs2;
-        const double R3 = fma(-r23, R2, fma(-r13, R1, fma(-r03, R0, V[3]))) * rs3;
-        const double W0 = X[0] * rs0;
-        const double W1 = fma(-r01, W0, X[1]) * rs1;
-        const double W2 = fma(-r12, W1, fma(-r02, W0, X[2])) * rs2;
-        const double W3 = fma(-r23, W2, fma(-r13, W1, fma(-r03, W0, X[3]))) * rs3;
-        R = g == 0 ? R0 : (g == 1 ? R1 : (g == 2 ? R2 : R3));
-        Wb = g == 0 ? W0 : (g == 1 ? W1 : (g == 2 ? W2 : W3));
-      }
-#endif
-      hook.template run<B>();  // independent MFMA work interleaved with the chain
-      W[B] = Wb;
-      if constexpr (B < 3) {
-        const d4 t = __builtin_amdgcn_mfma_f64_16x16x4f64(R, R, Dt, 0, 0, 1);   // Dt -= R'R
-        const d4 u = __builtin_amdgcn_mfma_f64_16x16x4f64(R, Wb, It, 0, 0, 1);  // It -= R'W
-#pragma unroll
-        for (int r = B + 1; r < 4; ++r) {
-          Dt[r] = t[r];
-          It[r] = u[r];
-        }
-      }
-      tile_block<B + 1>(Dt, It, W, ok, hook);
-    }
-  }
-  template <class H = NoHook>
-  __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok, const H& hook = H()) const {
-    MARK_BEGIN("factor_tile");
-    LANE_IDS();
-    d4 It;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) It[r] = (g + 4 * r == cl) ? 1.0 : 0.0;
-    W = It;
-    tile_block<0>(Dt, It, W, ok, hook);
   }
 
   // tile transpose: by MFMA against the identity (X' I), no LDS hand-off, or
