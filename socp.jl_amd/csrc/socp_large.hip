@@ -84,6 +84,14 @@ __device__ __forceinline__ double wave_sum(double v) {
   dpp_scan<1>(x, (int)(threadIdx.x & 63), 0, false);
   return readlane_d(x[0], 63);
 }
+// sum over each 16-lane row (every lane of the row gets it): DPP rotations
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_all<0x128>(v);  // row_ror:8
+  v += dpp_all<0x124>(v);  // row_ror:4
+  v += dpp_all<0x122>(v);  // row_ror:2
+  v += dpp_all<0x121>(v);  // row_ror:1
+  return v;
+}
 __device__ __forceinline__ double wave_max(double v) {
   double x[1] = {v};
   dpp_scan<1>(x, (int)(threadIdx.x & 63), 0, true);
@@ -92,6 +100,9 @@ __device__ __forceinline__ double wave_max(double v) {
 
 #ifndef SOCP_LG_PANEL
 #define SOCP_LG_PANEL 1  // 0: the per-pivot rank-1 sweep of a panel (A/B builds)
+#endif
+#ifndef SOCP_LG_CHOL
+#define SOCP_LG_CHOL 1  // 0: Li = H^-1 by the Gauss-Jordan sweep (A/B builds)
 #endif
 
 // C += U'V (NEG = 1: C -= U'V) for C/D-layout 16x16 tiles (socp_small.hpp's
@@ -654,7 +665,7 @@ struct Large {
   // column-major read-modify-write of the block is 128 contiguous bytes per
   // 16 lanes (load_blkT / store_blkT) instead of 32 bytes over 16 columns.
   // LO (diagonal block): tiles with b < a lie above the diagonal (skipped).
-  template <bool LO = false>
+  template <bool LO = false, bool FV = true>
   __device__ __forceinline__ void gram_blkT(d4 (&acc)[4][4], gcdbl* Y, int ld, int I0, int J0, gcdbl* fv) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll 1
@@ -663,7 +674,7 @@ struct Large {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         gcdbl* row = Y + (int64_t)(k0 + 4 * s + g) * ld;
-        const double f = fv[k0 + 4 * s + g];
+        const double f = FV ? fv[k0 + 4 * s + g] : 1.0;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           av[t][s] = f * row[J0 + 16 * t + cl];
@@ -914,7 +925,11 @@ struct Large {
   // Wave w holds tile columns j = w + 8i of the panel's four tile rows; each
   // of the 4 + 4 steps publishes the tiles the others need through four LDS
   // tile slots at o_row (8 LDS barriers per panel instead of 64 pivot steps).
-  template <int nb>
+  // CHOL: the Cholesky factorisation's panel instead (chol_nb): the columns
+  // left of the panel are not touched, and after the forward pass the panel
+  // is stored in place -- Y = L_PP^-1 M_P,J = L_JP' (J > P) as columns of L,
+  // and E = L_PP^-1 in the diagonal block (lower triangle, column-major).
+  template <int nb, bool CHOL = false>
   __device__ __forceinline__ bool panel_tiles(gdbl* M, int ld, int P) {
     constexpr int NT = 4 * nb, NJ = (NT + NW - 1) / NW;
     const int w = wv, RW = L.RW, P0 = 64 * P, ob = L.o_row, of = L.o_rv;
@@ -931,7 +946,7 @@ struct Large {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int x = P0 + 16 * t + g + 4 * r, y = 16 * j + cl;  // element (x, y), lower triangle
-            R[t][i][r] = j < NT ? M[(y <= x) ? (int64_t)y * ld + x : (int64_t)x * ld + y] : 0.0;
+            R[t][i][r] = (j < NT && (!CHOL || j >= 4 * P)) ? M[(y <= x) ? (int64_t)y * ld + x : (int64_t)x * ld + y] : 0.0;
           }
       }
     }
@@ -976,7 +991,7 @@ struct Large {
 #pragma unroll
       for (int i = 0; i < NJ; ++i) {
         const int j = w + NW * i;
-        if (j >= NT || j == jd) continue;
+        if (j >= NT || j == jd || (CHOL && j < 4 * P)) continue;
         const int u = ((j >> 2) == P) ? (j & 3) : -1;  // P-block tile column index
         d4 X = (u >= 0 && u < t) ? zero : R[t][i];      // E: the identity's zero below
 #pragma unroll
@@ -990,6 +1005,27 @@ struct Large {
 #pragma unroll
     for (int t = 0; t < 4; ++t) ok = ok && LV(of + t) == 0.0;
     if (!ok) return false;  // uniform: every wave read the same flags
+    if constexpr (CHOL) {
+      LANE_IDS();
+#pragma unroll
+      for (int i = 0; i < NJ; ++i) {
+        const int j = w + NW * i;
+        if (j >= NT || j < 4 * P) continue;
+        const bool pb = (j >> 2) == P;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int x = P0 + 16 * t + g + 4 * r, y = 16 * j + cl;  // tile element (x, y)
+            if (!pb)
+              M[(int64_t)x * ld + y] = R[t][i][r];  // L[y][x]: column x of L, coalesced
+            else if ((j & 3) <= t && y <= x)
+              M[(int64_t)y * ld + x] = R[t][i][r];  // E[x][y]
+          }
+      }
+      if (tid < 64) Rv[P0 + tid] = -1.0;
+      return true;
+    }
     {
       // the Gram updates' rows: Y off the P block, and fv = -1 (rows are L^-1-scaled)
       LANE_IDS();
@@ -1061,6 +1097,133 @@ struct Large {
       }
     }
     return true;
+  }
+
+  // In-place blocked Cholesky H = L L' (densesolver.jl:47 cholesky!; the
+  // explicit Li = H^-1 of :48 is never formed, its products are triangular
+  // solves against L -- see solve_matrix_part).  Left-looking by 64-column
+  // panels: block (t, P), t >= P, first receives the Gram updates of the
+  // panels Q < P (its columns of L read as rows: column x of L is contiguous),
+  // then panel_tiles<CHOL> factors the pivot block by 16x16 tiles and stores
+  // L_JP and E_P = L_PP^-1.  A pivot <= 0 or NaN fails as potrf does.
+  template <int nb>
+  __device__ bool chol_nb(gdbl* M, int ld) {
+    for (int P = 0; P < nb; ++P) {
+      if (P > 0) {
+        for (int t = P + wv; t < nb; t += NW) {
+          d4 acc[4][4];
+          if (t == P) {
+            load_blkT<true>(acc, M, ld, 64 * t, 64 * P);
+            for (int Q = 0; Q < P; ++Q) gram_blkT<true>(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q);
+            store_blkT<true>(acc, M, ld, 64 * t, 64 * P);
+          } else {
+            load_blkT(acc, M, ld, 64 * t, 64 * P);
+            for (int Q = 0; Q < P; ++Q) gram_blkT(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q);
+            store_blkT(acc, M, ld, 64 * t, 64 * P);
+          }
+        }
+        BAR();
+      }
+      LSTAMP(NSTAMP + 1 + 0);
+      const bool ok = panel_tiles<nb, true>(M, ld, P);
+      LSTAMP(NSTAMP + 1 + 1);
+      if (!ok) return false;
+      BAR();  // L's panel P complete before the next catch-up reads it
+      LSTAMP(NSTAMP + 1 + 2);
+    }
+    return true;
+  }
+  __device__ bool chol(gdbl* M, int ld) {
+    switch (ld / 64) {
+      case 1: return chol_nb<1>(M, ld);
+      case 2: return chol_nb<2>(M, ld);
+      case 3: return chol_nb<3>(M, ld);
+      case 4: return chol_nb<4>(M, ld);
+      case 5: return chol_nb<5>(M, ld);
+      case 6: return chol_nb<6>(M, ld);
+      case 7: return chol_nb<7>(M, ld);
+      default: return chol_nb<8>(M, ld);
+    }
+  }
+
+  // Z = L^-1 A' (NPAD x MPAD, row-major in Tm) by block forward substitution:
+  // Z_P = E_P (A'_P - sum_{y < 64P} L[P rows][y] Z[y]), 16x16 output tiles
+  // dealt over the wavefronts (MFMA: A operand = L / E read down a column,
+  // B operand = rows of Z); R = A'_P - ... is staged in Yp (row-major 64 x
+  // MPAD) between the two products.
+  __device__ void chol_fwd_multi(gcdbl* Lm, int ld) {
+    const int NB = L.NPAD / 64, MT = L.MPAD / 16, MP = L.MPAD;
+    gdbl* const Rs = Yp;
+    const d4 zero = {0.0, 0.0, 0.0, 0.0};
+    for (int P = 0; P < NB; ++P) {
+      const int P0 = 64 * P;
+      for (int tt = wv; tt < 4 * MT; tt += NW) {
+        LANE_IDS();
+        const int ta = tt / MT, tb = tt - ta * MT;
+        d4 acc0, acc1 = zero;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc0[r] = Ap[(int64_t)(P0 + 16 * ta + g + 4 * r) * MP + 16 * tb + cl];
+        for (int y0 = 0; y0 < P0; y0 += 8) {
+          const double a0 = Lm[(int64_t)(y0 + g) * ld + P0 + 16 * ta + cl];
+          const double b0 = Tm[(int64_t)(y0 + g) * MP + 16 * tb + cl];
+          const double a1 = Lm[(int64_t)(y0 + 4 + g) * ld + P0 + 16 * ta + cl];
+          const double b1 = Tm[(int64_t)(y0 + 4 + g) * MP + 16 * tb + cl];
+          acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc0, 0, 0, 1);  // -= L Z
+          acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc1, 0, 0, 1);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Rs[(int64_t)(16 * ta + g + 4 * r) * MP + 16 * tb + cl] = acc0[r] + acc1[r];
+      }
+      BAR();
+      for (int tt = wv; tt < 4 * MT; tt += NW) {
+        LANE_IDS();
+        const int ta = tt / MT, tb = tt - ta * MT, i = 16 * ta + cl;
+        d4 acc = zero;
+        for (int x0 = 0; x0 <= 16 * ta + 12; x0 += 4) {  // E is lower: x <= i
+          const int x = x0 + g;
+          const double av = (x <= i) ? Lm[(int64_t)(P0 + x) * ld + P0 + i] : 0.0;
+          const double bv = Rs[(int64_t)x * MP + 16 * tb + cl];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Tm[(int64_t)(P0 + 16 * ta + g + 4 * r) * MP + 16 * tb + cl] = acc[r];
+      }
+      BAR();
+    }
+  }
+
+  // S = Z'Z = A Li A' (lower 64x64 blocks; the padded diagonal gets the
+  // identity, as store_blk's)
+  __device__ void form_S_gram() {
+    const int NB = L.NPAD / 64, MB = L.MPAD / 64, MP = L.MPAD;
+    for (int t = wv; t < MB * (MB + 1) / 2; t += NW) {
+      LANE_IDS();
+      int I, J;
+      tri_ij(t, I, J);
+      d4 acc[4][4];
+      zero_blk(acc);
+      for (int P = 0; P < NB; ++P) {
+        if (I == J)
+          gram_blkT<true, false>(acc, Tm + (int64_t)64 * P * MP, MP, 64 * I, 64 * J, nullptr);
+        else
+          gram_blkT<false, false>(acc, Tm + (int64_t)64 * P * MP, MP, 64 * I, 64 * J, nullptr);
+      }
+      if (I == J) {
+#pragma unroll
+        for (int a_ = 0; a_ < 4; ++a_)
+#pragma unroll
+          for (int b_ = 0; b_ < 4; ++b_)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = 64 * I + 16 * b_ + cl, col = 64 * J + 16 * a_ + g + 4 * r;
+              if (row == col && row >= m) acc[a_][b_][r] = 1.0;
+            }
+        store_blkT<true>(acc, Sm, MP, 64 * I, 64 * J);
+      } else {
+        store_blkT(acc, Sm, MP, 64 * I, 64 * J);
+      }
+    }
+    BAR();
   }
 
   // Blocked symmetric Gauss-Jordan sweep of the 64nb x 64nb symmetric matrix
@@ -1278,6 +1441,14 @@ struct Large {
     LSTAMP(SP_U);
     form_H(addAA);
     LSTAMP(SP_SYRK);
+#if SOCP_LG_CHOL
+    if (!chol(Hm, L.NPAD)) return ST_CHOL_H;
+    if (h_only) return 0;
+    LSTAMP(SP_SWEEP_H);
+    chol_fwd_multi(Hm, L.NPAD);
+    form_S_gram();
+    LSTAMP(SP_SCHUR);
+#else
     if (!sweep(Hm, L.NPAD)) return ST_CHOL_H;
     if (h_only) return 0;
     LSTAMP(SP_SWEEP_H);
@@ -1303,6 +1474,7 @@ struct Large {
     }
     BAR();
     LSTAMP(SP_SCHUR);
+#endif
     if (!sweep(Sm, L.MPAD)) return ST_CHOL_S;
     finalize_sym(Sm, L.MPAD);
     LSTAMP(SP_SCHUR);
@@ -1352,11 +1524,13 @@ struct Large {
     for (int r = 0; r < m; ++r) acc = fma(At[(int64_t)r * L.NPAD + j], LV(v + r), acc);
     return acc;
   }
-  // out[r] = (A u)[r] - sub[r] for r < m; returns this thread's share of |out|^2
-  __device__ double A_mv(int u, int sub, int out) {
+  // out[r] = (A u)[r] - sub[r] for r < m; returns this thread's share of |out|^2.
+  // Mt: A' row-major (Ap), or Z = L^-1 A' (Tm, the Cholesky path): out = Z'u - sub.
+  __device__ double A_mv(int u, int sub, int out) { return mat_mv(Ap, u, sub, out); }
+  __device__ double mat_mv(gcdbl* Mt, int u, int sub, int out) {
     for (int r = lane; r < L.MPAD; r += 64) {
       double acc = 0.0;
-      for (int j = wv; j < n; j += NW) acc = fma(Ap[(int64_t)j * L.MPAD + r], LV(u + j), acc);
+      for (int j = wv; j < n; j += NW) acc = fma(Mt[(int64_t)j * L.MPAD + r], LV(u + j), acc);
       LV(L.o_part + wv * L.MPAD + r) = acc;
     }
     BAR();
@@ -1383,6 +1557,85 @@ struct Large {
     }
     BAR();
     LSTAMP(NSTAMP + 1 + 6);
+  }
+
+  // Triangular solves against the in-place factor of chol_nb (L below the
+  // diagonal blocks, E_P = L_PP^-1 in them), 64 rows per step.  Rows >= n
+  // (padding) are never read.
+  // out = L^-1 in: r = in_P - L_P,<P out_<P (lanes = rows, wavefronts split
+  // the columns; partial sums through LDS), out_P = E_P r.
+  __device__ void trsv_fwd(gcdbl* Lm, int ld, int vin, int vout) {
+    const int NB = L.NPAD / 64, p1 = L.o_part, p2 = L.o_fx;
+    LSTAMP(SP_SOLVE);
+    for (int P = 0; P < NB; ++P) {
+      const int P0 = 64 * P, i = P0 + lane;
+      double acc = 0.0;
+      if (i < n) {
+#pragma unroll 8
+        for (int y = wv; y < P0; y += NW) acc = fma(Lm[(int64_t)y * ld + i], LV(vout + y), acc);
+      }
+      LV(p1 + wv * 64 + lane) = acc;
+      LDS_BAR();
+      acc = 0.0;
+      for (int x = wv; x < 64 && P0 + x < n; x += NW) {
+        double r = LV(vin + P0 + x);
+#pragma unroll
+        for (int w = 0; w < NW; ++w) r -= LV(p1 + w * 64 + x);
+        if (x <= lane && i < n) acc = fma(Lm[(int64_t)(P0 + x) * ld + i], r, acc);
+      }
+      LV(p2 + wv * 64 + lane) = acc;
+      LDS_BAR();
+      if (wv == 0 && i < n) {
+        double u = 0.0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) u += LV(p2 + w * 64 + lane);
+        LV(vout + i) = u;
+      }
+      LDS_BAR();
+    }
+    LSTAMP(NSTAMP + 1 + 6);
+  }
+  // out = L^-T in, last block first: r = in_P - L_>P,P' out_>P, out_P = E_P' r.
+  // Both products read columns of L / E (contiguous): 16 lanes per column,
+  // four columns per wavefront step.
+  __device__ void trsv_bwd(gcdbl* Lm, int ld, int vin, int vout) {
+    const int NB = L.NPAD / 64, p1 = L.o_part, q = lane >> 4, c = lane & 15;
+    LSTAMP(SP_SOLVE);
+    for (int P = NB - 1; P >= 0; --P) {
+      const int P0 = 64 * P;
+      for (int i = 4 * wv + q; i < 64; i += 4 * NW) {
+        double acc = 0.0;
+        for (int x = P0 + 64 + c; x < n; x += 16) acc = fma(Lm[(int64_t)(P0 + i) * ld + x], LV(vout + x), acc);
+        acc = row16_sum(acc);
+        if (c == 0) LV(p1 + i) = (P0 + i < n) ? LV(vin + P0 + i) - acc : 0.0;
+      }
+      LDS_BAR();
+      for (int i = 4 * wv + q; i < 64; i += 4 * NW) {
+        double acc = 0.0;
+#pragma unroll
+        for (int s_ = 0; s_ < 4; ++s_) {
+          const int x = c + 16 * s_;
+          if (x >= i && P0 + x < n) acc = fma(Lm[(int64_t)(P0 + i) * ld + P0 + x], LV(p1 + x), acc);
+        }
+        acc = row16_sum(acc);
+        if (c == 0 && P0 + i < n) LV(vout + P0 + i) = acc;
+      }
+      LDS_BAR();
+    }
+    LSTAMP(NSTAMP + 1 + 6);
+  }
+  // out[j] = u[j] + (Z m)[j], j < n (Z row-major in Tm: 16 lanes per row)
+  __device__ void z_mv_add(int u, int mv, int out) {
+    const int q = lane >> 4, c = lane & 15;
+    for (int j0 = 4 * wv; j0 < n; j0 += 4 * NW) {
+      const int j = j0 + q;
+      double acc = 0.0;
+      if (j < n)
+        for (int r = c; r < m; r += 16) acc = fma(Tm[(int64_t)j * L.MPAD + r], LV(mv + r), acc);
+      acc = row16_sum(acc);
+      if (c == 0 && j < n) LV(out + j) = LV(u + j) + acc;
+    }
+    LDS_BAR();
   }
 
   // rd = A'y + G'z + c, rp = Ax - b, rz = Gx + s - h (solver.jl:109-118)
@@ -1413,6 +1666,17 @@ struct Large {
       for (int j = tid; j < n; j += NTH) LV(N0 + j) = LV(N0 + j) + At_dot(RP, j);
       BAR();
     }
+#if SOCP_LG_CHOL
+    // Li = L^-T L^-1: u = L^-1 n0; m0 = A Li n0 - dy = Z'u - dy; cy = S^-1 m0;
+    // cx = Li (n0 + A'm0) = L^-T (u + Z m0)
+    trsv_fwd(Hm, L.NPAD, N0, TN);
+    mat_mv(Tm, TN, RP, M0);
+    symv(Sm, L.MPAD, M0, RY);
+    for (int r = tid; r < m; r += NTH) LV(M0 + r) = (sing && !init) ? LV(RP + r) - LV(RY + r) : -LV(RY + r);
+    BAR();
+    z_mv_add(TN, M0, N0);
+    trsv_bwd(Hm, L.NPAD, N0, RX);
+#else
     symv(Hm, L.NPAD, N0, TN);
     A_mv(TN, RP, M0);
     symv(Sm, L.MPAD, M0, RY);
@@ -1426,6 +1690,7 @@ struct Large {
       LV(RX + j) = LV(TN + j) + acc;
     }
     BAR();
+#endif
     gemv_G(RX, -1, K2, K1);
   }
 
