@@ -47,6 +47,7 @@ class Params(C.Structure):
 
 F_WARM_START = 2
 F_STRUCTURED = 16  # oracle-only: the build's structured algorithm (CPU baseline line)
+F_CHOLSOLVE = 64  # oracle-only, with F_STRUCTURED: Li v by triangular solves, S = Z'Z (the register kernel at m <= 16)
 F_SQR = 32  # oracle-only: SqrScaling + SparseSolver (spsolver.jl, the rank-update path)
 
 
@@ -163,10 +164,12 @@ def scale(cones, wbs, mu, x, inverse=False):
     return out
 
 
-def kkt_single(cones, A, G, sing, s, z, dx, dy, dz, ds, want_H=False, structured=False):
+def kkt_single(cones, A, G, sing, s, z, dx, dy, dz, ds, want_H=False, structured=False, chol=False):
     """compute_scaling + setup_iter + solve_kkt (densesolver.jl:41-90) at iterate (s,z).
     structured: the kernels' order (X = W^-1 G per cone, H = X'X; F_STRUCTURED)
-    instead of the reference's (dense iW*iW', G'*iWiW*G); no H output then."""
+    instead of the reference's (dense iW*iW', G'*iWiW*G); no H output then.
+    chol (with structured): no explicit Li -- Z = L^-1 A', S = Z'Z and the
+    triangular solves the register kernel runs for m <= 16 (F_CHOLSOLVE)."""
     A = np.asarray(A, dtype=np.float64).reshape(-1, G.shape[1]) if np.size(A) else np.zeros((0, G.shape[1]))
     m, n = A.shape
     k = G.shape[0]
@@ -177,7 +180,7 @@ def kkt_single(cones, A, G, sing, s, z, dx, dy, dz, ds, want_H=False, structured
                              _f(G.ravel(order="F")), int(sing), _f(s), _f(z), _f(dx),
                              _f(dy) if m else np.zeros(1), _f(dz), _f(ds), cx, cy if m else np.zeros(1), cz, cs,
                              H.ctypes.data if want_H else None, Li.ctypes.data if want_H else None,
-                             int(bool(structured)))
+                             int(bool(structured)) | (2 if (structured and chol) else 0))
     out = dict(cx=cx, cy=cy, cz=cz, cs=cs, status=st)
     if want_H:
         out["H"] = H.reshape(n, n, order="F")

@@ -382,6 +382,9 @@ static void potrs_u(const double* U, int n, double* b) {
 typedef struct {
   int n, m, k, sing;
   int structured;        /* OR_F_STRUCTURED: the build's algorithm, not the reference op order */
+  int cholsolve;         /* OR_F_CHOLSOLVE (with structured): no explicit Li -- Z = U^-T A' kept in
+                            ALi (as Z', m x n), S = Z'Z, Li v by the two triangular solves of potrs
+                            (the register kernel's order for m <= 16) */
   const cones_t* C;
   const double *A, *G; /* column-major m x n, k x n */
   double *AA, *GWiWi, *H, *Li, *ALi, *S;
@@ -423,6 +426,26 @@ static int setup_iter(dense_t* D, const scaling_t* S) {
   if (D->sing)
     for (size_t q = 0; q < (size_t)n * n; ++q) D->H[q] += D->AA[q];
   if (potrf_u(D->H, n)) return 2;
+  if (D->cholsolve) {
+    /* H = U'U: Z = U^-T A' column by column (Z' in ALi), S = Z'Z */
+    for (int r = 0; r < m; ++r) {
+      double* zr = D->n1; /* scratch */
+      for (int a = 0; a < n; ++a) {
+        double t = M(D->A, m, r, a);
+        for (int q = 0; q < a; ++q) t -= M(D->H, n, q, a) * zr[q];
+        zr[a] = t / M(D->H, n, a, a);
+      }
+      for (int a = 0; a < n; ++a) M(D->ALi, m, r, a) = zr[a];
+    }
+    for (int q = 0; q < m; ++q)
+      for (int r = 0; r < m; ++r) {
+        double acc = 0.0;
+        for (int a = 0; a < n; ++a) acc += M(D->ALi, m, r, a) * M(D->ALi, m, q, a);
+        M(D->S, m, r, q) = acc;
+      }
+    if (potrf_u(D->S, m)) return 3;
+    return 0;
+  }
   /* Li = H^-1 via ldiv!(Li, fact, I) */
   for (int j = 0; j < n; ++j) {
     double* col = D->Li + (size_t)j * n;
@@ -475,6 +498,12 @@ static void solve_kkt(dense_t* D, const cones_t* C, const scaling_t* S, const do
       for (int r = 0; r < m; ++r) acc += M(D->A, m, r, a) * dy[r];
       D->n0[a] += acc;
     }
+  if (D->cholsolve) /* t = U^-T n0 (the first half of potrs); A Li n0 = Z't */
+    for (int i = 0; i < n; ++i) {
+      double t = D->n0[i];
+      for (int q = 0; q < i; ++q) t -= M(D->H, n, q, i) * D->n0[q];
+      D->n0[i] = t / M(D->H, n, i, i);
+    }
   for (int r = 0; r < m; ++r) {
     double acc = 0.0;
     for (int a = 0; a < n; ++a) acc += M(D->ALi, m, r, a) * D->n0[a];
@@ -487,6 +516,19 @@ static void solve_kkt(dense_t* D, const cones_t* C, const scaling_t* S, const do
     for (int r = 0; r < m; ++r) D->m0[r] = dy[r] - cy[r];
   else
     for (int r = 0; r < m; ++r) D->m0[r] = -cy[r];
+  if (D->cholsolve) {
+    /* cx = U^-1 (t + Z m0) (the second half of potrs) */
+    for (int a = 0; a < n; ++a) {
+      double acc = 0.0;
+      for (int r = 0; r < m; ++r) acc += M(D->ALi, m, r, a) * D->m0[r];
+      cx[a] = D->n0[a] + acc;
+    }
+    for (int q = n - 1; q >= 0; --q) {
+      double t = cx[q];
+      for (int i = q + 1; i < n; ++i) t -= M(D->H, n, q, i) * cx[i];
+      cx[q] = t / M(D->H, n, q, q);
+    }
+  } else {
   for (int a = 0; a < n; ++a) {
     double acc = 0.0;
     for (int r = 0; r < m; ++r) acc += M(D->A, m, r, a) * D->m0[r];
@@ -497,6 +539,7 @@ static void solve_kkt(dense_t* D, const cones_t* C, const scaling_t* S, const do
     double acc = 0.0;
     for (int b = 0; b < n; ++b) acc += M(D->Li, n, a, b) * D->n0[b];
     cx[a] = acc;
+  }
   }
   for (int i = 0; i < k; ++i) {
     double acc = 0.0;
@@ -815,6 +858,7 @@ static int ws_init(ws_t* w, int n, int m, int k, int ncones, int maxdim) {
   w->D.m = m;
   w->D.k = k;
   w->D.structured = 0;
+  w->D.cholsolve = 0;
   w->D.C = NULL;
   w->D.AA = carve(&p, sizeof(double) * n * n);
   w->D.H = carve(&p, sizeof(double) * n * n);
@@ -901,6 +945,7 @@ typedef struct {
 #define F_WARM 2
 #define OR_F_STRUCTURED 16 /* oracle-only: the build's structured algorithm (CPU baseline) */
 #define OR_F_SQR 32        /* oracle-only: SqrScaling + SparseSolver (spsolver.jl) instead of DenseSolver */
+#define OR_F_CHOLSOLVE 64  /* oracle-only, with OR_F_STRUCTURED: triangular solves instead of the explicit Li */
 
 static double dot(const double* a, const double* b, int n) {
   double s = 0.0;
@@ -964,6 +1009,7 @@ static void solve_one(ws_t* w, const cones_t* C, const double* c, const double* 
   D->sing = sing;
   D->C = C;
   D->structured = (P->flags & OR_F_STRUCTURED) != 0;
+  D->cholsolve = D->structured && (P->flags & OR_F_CHOLSOLVE) != 0;
   const int sqr = (P->flags & OR_F_SQR) != 0;
 #define KKT(a, b_, c_, d, e, f, g, h_) \
   (sqr ? sqr_solve_kkt(D, C, S, a, b_, c_, d, e, f, g, h_) : solve_kkt(D, C, S, a, b_, c_, d, e, f, g, h_))
@@ -1180,8 +1226,10 @@ EXPORT int or_kkt_single(int nc, const int32_t* kind, const int32_t* offs, const
   w.D.G = G;
   w.D.sing = sing;
   w.D.C = &C;
-  w.D.structured = structured; /* the kernels' order (F_STRUCTURED); H output: reference order only */
+  w.D.structured = structured != 0; /* the kernels' order (F_STRUCTURED); H output: reference order only */
+  w.D.cholsolve = (structured & 2) != 0; /* 2 | 1: with the triangular solves (OR_F_CHOLSOLVE) */
   if (structured) Hout = NULL;
+  if (structured & 2) Liout = NULL;
   for (int bq = 0; bq < n; ++bq)
     for (int a = 0; a < n; ++a) {
       double acc = 0.0;

@@ -625,6 +625,13 @@ struct Small {
   // most 4 such tiles; larger ones take A'm0 and a second Li product)
   static constexpr bool KEEP_AL = SOCP_KEEP_AL && NQ * MQ <= 4;
   d4 AL[KEEP_AL ? MQ : 1][KEEP_AL ? NQ : 1];
+#ifndef SOCP_SMALL_CHOL
+#define SOCP_SMALL_CHOL 1  // 0: Li = H^-1 by the Gauss-Jordan sweep for every shape (A/B builds)
+#endif
+  // m <= 16: H = L L' (chol), Z = L^-1 A' in LDS, S = Z'Z; Li is never formed
+  // and its products are triangular solves (trsv_fwd / trsv_bwd).  Larger m
+  // keep the explicit inverse by the sweep.
+  static constexpr bool CHOL = SOCP_SMALL_CHOL && AL_LDS && !KEEP_AL;
 
   __device__ __forceinline__ Small(const SmallArgs& args)
       : a(args), lane(threadIdx.x), g(threadIdx.x >> 4), cl(threadIdx.x & 15),
@@ -1339,7 +1346,8 @@ struct Small {
 #pragma unroll
       for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
-        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = mfma(Xc[ti], Xc[tj], T[tri(ti, tj)]);
+        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = CHOL ? mfma(Xc[tj], Xc[ti], T[tri(ti, tj)])   // block (tj, ti)
+                                                                : mfma(Xc[ti], Xc[tj], T[tri(ti, tj)]);  // block (ti, tj)
       if (pp + 1 < NP) {
 #pragma unroll
         for (int r = 0; r < NT; ++r) {
@@ -1360,7 +1368,7 @@ struct Small {
 #pragma unroll
       for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
-        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = mfma(X[ti], X[tj], T[tri(ti, tj)]);
+        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = CHOL ? mfma(X[tj], X[ti], T[tri(ti, tj)]) : mfma(X[ti], X[tj], T[tri(ti, tj)]);
       if (pp % 2 == 1) SCHED_FENCE();
     }
 #endif
@@ -1376,7 +1384,7 @@ struct Small {
 #pragma unroll
           for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
-            for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = mfma(Aq[ti], Aq[tj], T[tri(ti, tj)]);
+            for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = CHOL ? mfma(Aq[tj], Aq[ti], T[tri(ti, tj)]) : mfma(Aq[ti], Aq[tj], T[tri(ti, tj)]);
         }
     }
 #pragma unroll
@@ -1542,6 +1550,118 @@ struct Small {
     return ok;
   }
 
+  // ------------------------------------ H = L L' by 16x16 tiles (CHOL shapes)
+  // densesolver.jl:47 cholesky!(Hermitian(H)), right-looking by tile panels.
+  // The explicit Li of :48 is never formed: ALi = A Li enters as Z = L^-1 A'
+  // (S = A Li A' = Z'Z, :49-50) and Li v as two triangular solves.  Storage:
+  // the SYRK leaves block (i, j), i <= j, of H in T[tri(j, i)] (upper tiles),
+  // so the panel row U_Pi needs no transpose; after panel P, T[tri(P, P)]
+  // holds W_P = L_PP^-1 (factor_tile) and T[tri(i, P)] = L_iP' (i > P).
+  // Panel P: Y_i = W_P U_Pi = L_iP' (MFMA), U_ij -= Y_i'Y_j (P < i <= j).
+  // Look-ahead: Y_{P+1} and U_{P+1,P+1} first, then the next pivot tile is
+  // factored with the rest of the panel's MFMA work -- and the panel's tile
+  // row of Z -- dealt out between its row blocks.  Every pivot is a Cholesky
+  // pivot of H (potrf's test, as the sweep's).
+  struct CholOp {
+    int kind, i, j;  // 0: Y_i = W_P U_Pi, 1: U_ij -= Y_i'Y_j, 2: the Z row of panel P, -1: none
+  };
+  template <int P>
+  static constexpr CholOp chol_op(int idx) {
+    int cnt = 0;
+    for (int i = P + 2; i < NQ; ++i)
+      if (cnt++ == idx) return CholOp{0, i, 0};
+    for (int j = P + 1; j < NQ; ++j)  // column-major: U_{P+1,P+2} and U_{P+2,P+2} (the next panel's) first
+      for (int i = P + 1; i <= j; ++i) {
+        if (i == P + 1 && j == P + 1) continue;
+        if (cnt++ == idx) return CholOp{1, i, j};
+      }
+    if (cnt++ == idx) return CholOp{2, P, 0};
+    return CholOp{-1, 0, 0};
+  }
+  template <int P>
+  static constexpr int chol_op_count() {
+    int c = 0;
+    while (chol_op<P>(c).kind >= 0) ++c;
+    return c;
+  }
+  // Z_P = W_P (A'_P - sum_{Q<P} L_PQ Z_Q) (left-looking: one accumulator tile),
+  // S += Z_P'Z_P (Sv[0]); Z' row-major in LDS at O_AL (where the sweep path
+  // keeps A Li): Z'[c][j] = LDS(O_AL + c*LDA + j).
+  template <int P>
+  __device__ __forceinline__ void z_row(const d4& WT) {
+    LANE_IDS();
+    SYNC();
+    d4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = LDS(O_A + cl * LDA + 16 * P + g + 4 * r);  // A'[16P+g+4r][cl]
+#pragma unroll
+    for (int Q = 0; Q < P; ++Q) {
+      d4 Zq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Zq[r] = LDS(O_AL + cl * LDA + 16 * Q + g + 4 * r);
+      acc = mm<1>(T[tri(P, Q)], Zq, acc);  // -= L_PQ Z_Q
+    }
+    const d4 Z = mm<0>(WT, acc, (d4){0.0, 0.0, 0.0, 0.0});
+    Sv[0] = mm<0>(Z, Z, Sv[0]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) LDS(O_AL + cl * LDA + 16 * P + g + 4 * r) = Z[r];
+  }
+  template <int P, int OP>
+  __device__ __forceinline__ void chol_op_run(const d4& WT) {
+    constexpr CholOp o = chol_op<P>(OP);
+    if constexpr (o.kind == 0) {
+      T[tri(o.i, P)] = mm<0>(WT, T[tri(o.i, P)], (d4){0.0, 0.0, 0.0, 0.0});
+    } else if constexpr (o.kind == 1) {
+      T[tri(o.j, o.i)] = mm<1>(T[tri(o.i, P)], T[tri(o.j, P)], T[tri(o.j, o.i)]);
+    } else if constexpr (o.kind == 2) {
+      z_row<P>(WT);
+    }
+  }
+  template <int P, int LO, int HI>
+  __device__ __forceinline__ void chol_ops(const d4& WT) {
+    if constexpr (LO < HI) {
+      chol_op_run<P, LO>(WT);
+      chol_ops<P, LO + 1, HI>(WT);
+    }
+  }
+  template <int P>
+  struct CholHook {
+    Small& s;
+    const d4& WT;
+    template <int B>
+    __device__ __forceinline__ void run() const {
+      constexpr int N = chol_op_count<P>();
+      s.template chol_ops<P, (N * B) / 4, (N * (B + 1)) / 4>(WT);
+    }
+  };
+  template <int P>
+  __device__ __forceinline__ void chol_panel(const d4& W, bool& ok) {
+    if constexpr (P < NQ) {
+      MARK_BEGIN("chol_panel");
+      const d4 WT = transpose(W);
+      if constexpr (P + 1 < NQ) {
+        T[tri(P + 1, P)] = mm<0>(WT, T[tri(P + 1, P)], (d4){0.0, 0.0, 0.0, 0.0});
+        T[tri(P + 1, P + 1)] = mm<1>(T[tri(P + 1, P)], T[tri(P + 1, P)], T[tri(P + 1, P + 1)]);
+        d4 Wn;
+        factor_tile(T[tri(P + 1, P + 1)], Wn, ok, CholHook<P>{*this, WT});
+        T[tri(P, P)] = W;
+        chol_panel<P + 1>(Wn, ok);
+      } else {
+        z_row<P>(WT);
+        T[tri(P, P)] = W;
+      }
+    }
+  }
+  __device__ __forceinline__ bool chol() {
+    Sv[0] = (d4){0.0, 0.0, 0.0, 0.0};
+    bool ok = true;
+    d4 W;
+    factor_tile(T[tri(0, 0)], W, ok);
+    chol_panel<0>(W, ok);
+    SYNC();
+    return ok;
+  }
+
   __device__ __forceinline__ d4 transpose(d4 t) {
     MARK_BEGIN("transpose");
     LANE_IDS();
@@ -1583,8 +1703,21 @@ struct Small {
 #ifdef SOCP_DIAG
     // diagnostic dump per problem: H, H^-1 (n x n each), lam, wbar (k each), Li A' (n x m), S (m x m)
     double* dbg = (a.dbg && a.mode == MODE_KKT) ? a.dbg + dbg_p * (int64_t)(2 * n * n + 2 * k + n * m + m * m) : nullptr;
-    if (dbg) dump_sym(dbg);
+    if (dbg && !CHOL) dump_sym(dbg);
 #endif
+    if constexpr (CHOL) {
+      const bool okH = chol();
+      STAMP(SP_SWEEP_H);
+      if (!okH) return ST_CHOL_H;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (g + 4 * r == cl && cl >= m) Sv[0][r] = 1.0;
+      const bool okS = sweep<1, false>(Sv);
+      STAMP(SP_SCHUR);
+      if (!okS) return ST_CHOL_S;
+      Sv[0] = -Sv[0];
+      return 0;
+    }
     const bool okH = sweep<NQ, true>(T);
     STAMP(SP_SWEEP_H);
     if (!okH) return ST_CHOL_H;
@@ -1731,6 +1864,84 @@ struct Small {
     if (g == 0) {
 #pragma unroll
       for (int t = 0; t < Q; ++t) LDS(vout + 16 * t + cl) += P2[t];
+    }
+    SYNC();
+  }
+
+  // Triangular solves against chol()'s factor (T[tri(P, P)] = W_P = L_PP^-1,
+  // T[tri(i, P)] = L_iP').  Tile products alternate between the two vector
+  // layouts of a C/D tile, so no LDS round trip sits on the chain: W v
+  // (v[cl] in every lane of column cl) gives (W v)[g+4r] after a 16-lane
+  // all-reduce; M'u (u[g+4r] in the lanes of row group g) gives (M'u)[cl]
+  // after the four-row sum.  The off-diagonal products of earlier tiles are
+  // accumulated lane-locally and reduced once per tile.
+  __device__ __forceinline__ static void allred16(double (&v)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += row_partner<8>(v[r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += row_partner<4>(v[r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += row_partner<2>(v[r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += row_partner<1>(v[r]);
+  }
+  // out = L^-1 v: t_P = W_P (v_P - sum_{Q<P} L_PQ t_Q)
+  __device__ __forceinline__ void trsv_fwd(int vin, int vout) {
+    MARK_BEGIN("trsv_fwd");
+    LANE_IDS();
+    double rc[NQ], pa[NQ];  // v (column layout), lane partials of sum_Q L_iQ t_Q
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      rc[i] = LDS(vin + 16 * i + cl);
+      pa[i] = 0.0;
+    }
+#pragma unroll
+    for (int P = 0; P < NQ; ++P) {
+      const double rp = P > 0 ? rc[P] - rows_sum(pa[P]) : rc[P];
+      double t4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t4[r] = T[tri(P, P)][r] * rp;
+      allred16(t4);  // t_P[g+4r]
+#pragma unroll
+      for (int i = P + 1; i < NQ; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pa[i] = fma(T[tri(i, P)][r], t4[r], pa[i]);
+      if (cl < 4) LDS(vout + 16 * P + g + 4 * cl) = cl == 0 ? t4[0] : (cl == 1 ? t4[1] : (cl == 2 ? t4[2] : t4[3]));
+    }
+    SYNC();
+  }
+  // out = L^-T v: x_P = W_P' (v_P - sum_{i>P} L_iP' x_i); in place is allowed
+  __device__ __forceinline__ void trsv_bwd(int vin, int vout) {
+    MARK_BEGIN("trsv_bwd");
+    LANE_IDS();
+    double ur[NQ][4], pa[NQ][4], xs[NQ];  // v (row layout), lane partials of sum_i L_iP' x_i
+#pragma unroll
+    for (int P = 0; P < NQ; ++P)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ur[P][r] = LDS(vin + 16 * P + g + 4 * r);
+        pa[P][r] = 0.0;
+      }
+#pragma unroll
+    for (int P = NQ - 1; P >= 0; --P) {
+      double u4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) u4[r] = pa[P][r];
+      if (P < NQ - 1) allred16(u4);
+      double acc = 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = fma(T[tri(P, P)][r], P < NQ - 1 ? ur[P][r] - u4[r] : ur[P][r], acc);
+      const double x = rows_sum(acc);  // x_P[cl]
+      xs[P] = x;
+#pragma unroll
+      for (int Q = 0; Q < P; ++Q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pa[Q][r] = fma(T[tri(P, Q)][r], x, pa[Q][r]);
+    }
+    SYNC();
+    if (g == 0) {
+#pragma unroll
+      for (int P = 0; P < NQ; ++P) LDS(vout + 16 * P + cl) = xs[P];
     }
     SYNC();
   }
@@ -1884,9 +2095,14 @@ struct Small {
     }
     SYNC();
     STAMP_X(4);
-    symv<NQ>(T, N0, TN);   // Li n0
+    if constexpr (CHOL)
+      trsv_fwd(N0, TN);    // t = L^-1 n0
+    else
+      symv<NQ>(T, N0, TN);   // Li n0
     STAMP_X(5);
-    if constexpr (AL_LDS)
+    if constexpr (CHOL)
+      A_mv(TN, RP, M0, O_AL);  // m0 = A Li n0 - dy = Z't - dy
+    else if constexpr (AL_LDS)
       A_mv(N0, RP, M0, O_AL);  // m0 = (A Li) n0 - dy: no wait for Li n0
     else
       A_mv(TN, RP, M0);        // m0 = A (Li n0) - dy
@@ -1900,6 +2116,7 @@ struct Small {
       ALt_mv(M0, TN, RX);
     } else if constexpr (AL_LDS) {
       // cx = Li (n0 + A'm0) = Li n0 + (A Li)' m0: one Li product per solve
+      // (CHOL: cx = L^-T (t + Z m0))
       double at[NQ];
       At_mv(M0, at, O_AL);
       if (g == 0) {
@@ -1907,6 +2124,7 @@ struct Small {
         for (int q = 0; q < NQ; ++q) LDS(RX + 16 * q + cl) = LDS(TN + 16 * q + cl) + at[q];
       }
       SYNC();
+      if constexpr (CHOL) trsv_bwd(RX, RX);
       STAMP_X(7);
     } else {
       double at[NQ];

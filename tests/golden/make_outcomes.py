@@ -2,7 +2,9 @@
 first 4,096 C2 problems under the reference's stopping rule (solver.jl:105,122:
 maxit = 40, absolute tol = 1e-5), per problem: status, iterations, final
 ||rd||, ||rp||, z's -- once in the reference's operation order and once in the
-structured order the HIP kernels use (oracle flag F_STRUCTURED).  The GPU test
+structured order the HIP kernels use (oracle flag F_STRUCTURED), with the
+explicit inverse and -- as the register kernel runs C2 (m <= 16) -- with
+triangular solves (F_STRUCTURED | F_CHOLSOLVE).  The GPU test
 tests/test_gpu_outcomes.py compares the HIP histogram and per-problem outcomes
 with these (allowed gaps: DESIGN.md §9).
 
@@ -37,7 +39,8 @@ def main():
     out = {"_doc": __doc__.strip().splitlines()[0], "config": cfg.name, "seed": cfg.seed, "batch": B,
            "maxit": 40, "tol": 1e-5, "runs": {}}
     sing = np.zeros(B, np.uint8)  # the generator's G (k > n, uniform entries) has full column rank
-    for name, flags in (("reference_order", 0), ("structured", O.F_STRUCTURED)):
+    for name, flags in (("reference_order", 0), ("structured", O.F_STRUCTURED),
+                        ("structured_chol", O.F_STRUCTURED | O.F_CHOLSOLVE)):
         r = O.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"], sing=sing,
                           params=O.Params(maxit=40, tol=1e-5, flags=flags), nthreads=os.cpu_count())
         out["runs"][name] = {"status": b64(r["status"], "<i1"), "iters": b64(r["iters"], "<i1"),
