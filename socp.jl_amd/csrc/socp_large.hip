@@ -1483,8 +1483,47 @@ struct Large {
 
   // ------------------------------------------------------------ mat-vecs
   // out[j] = (G' vin)[j] (+ add[j]) for j < n: a wavefront takes CG columns
+  // Fast path (k <= 64 GT_R): a wavefront loads its CG columns whole -- every
+  // load of the pass in flight at once (GT_R x CG per lane) -- instead of one
+  // 64-row step of the CG columns per memory round trip.
+  static constexpr int GT_R = 10;
+#ifndef SOCP_LG_GT_FAST
+#define SOCP_LG_GT_FAST 1
+#endif
   __device__ void gemv_Gt(int vin, int vout, int vadd) {
     LSTAMP(SP_SOLVE);
+    if (SOCP_LG_GT_FAST && k <= 64 * GT_R) {
+      double vr[GT_R];
+#pragma unroll
+      for (int r = 0; r < GT_R; ++r) vr[r] = (lane + 64 * r < k) ? LV(vin + lane + 64 * r) : 0.0;
+      for (int j0 = CG * wv; j0 < n; j0 += CG * NW) {
+        gcdbl* g0 = Gp + (int64_t)j0 * k;
+        const int nl = n - j0;
+        double gv[CG][GT_R];
+#pragma unroll
+        for (int u = 0; u < CG; ++u)
+#pragma unroll
+          for (int r = 0; r < GT_R; ++r) {
+            const int row = lane + 64 * r;
+            gv[u][r] = (row < k) ? g0[(int64_t)(u < nl ? u : 0) * k + row] : 0.0;
+          }
+        double acc[CG];
+#pragma unroll
+        for (int u = 0; u < CG; ++u) {
+          acc[u] = 0.0;
+#pragma unroll
+          for (int r = 0; r < GT_R; ++r) acc[u] = fma(gv[u][r], vr[r], acc[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < CG; ++u) {
+          const double s = wave_sum(acc[u]);
+          if (lane == 0 && j0 + u < n) LV(vout + j0 + u) = (vadd >= 0) ? s + LV(vadd + j0 + u) : s;
+        }
+      }
+      BAR();
+      LSTAMP(NSTAMP + 1 + 5);
+      return;
+    }
     for (int j0 = CG * wv; j0 < n; j0 += CG * NW) {
       gcdbl* g0 = Gp + (int64_t)j0 * k;
       const int nl = n - j0;  // live columns u < nl (dead ones re-read column j0)

@@ -75,16 +75,20 @@ struct SmallArgs {
 
 // ------------------------------------------------------------ LDS layout
 // Fixed region (independent of the template shape):
+#ifdef SOCP_DIAG
+#define SOCP_NSTAMP_SLOTS 24
+#else
+#define SOCP_NSTAMP_SLOTS 0
+#endif
 enum : int {
-  O_RC = 0,                  // rcode[KMAX]: cone*4 + type (0 POC, 1 SOC head, 2 SOC tail, 3 pad)
-  O_COFF = O_RC + KMAX,      // cone offs[NCS]
+  O_COFF = 0,                // cone offs[NCS]
   O_CDIM = O_COFF + NCS,     // cone dim[NCS]
   O_CKIND = O_CDIM + NCS,    // cone kind[NCS]
   O_CC = O_CKIND + NCS,        // per-cone constants of the current scaling [NCC][NCS]
   O_PART = O_CC + 20 * NCS,    // segment partials [NVMAX = 6][NCS][2 slots] (zero where unused)
   O_TOTC = O_PART + 6 * NCS * 2,  // per-cone results [4][NCS]
-  O_STAMPS = O_TOTC + 4 * NCS,  // diagnostic build: per-phase cycle totals of this wave [24]
-  O_KV = O_STAMPS + 24         // 17 k-vectors, Shape::KS apart
+  O_STAMPS = O_TOTC + 4 * NCS,  // diagnostic build only: per-phase cycle totals of this wave [24]
+  O_FIXED = O_STAMPS + SOCP_NSTAMP_SLOTS  // then (Shape): rcode[KP], 17 k-vectors KS apart, ...
 };
 constexpr int NKV = 17;
 // per-cone constants (SOC cones), recomputed by every scaling:
@@ -99,9 +103,13 @@ constexpr int NKV = 17;
 enum : int { CC_MU, CC_IMU, CC_WB0, CC_I1, CC_W2, CC_L0, CC_AA, CC_IAA, CC_IL0, CC_IL0AA, CC_SA,
              CC_SAL, CC_WL, CC_AS, CC_AZ, CC_BS, CC_BZ, CC_DLT, CC_KK };
 __host__ __device__ constexpr int cc(int q, int c) { return O_CC + q * NCS + c; }
-// k-vector ids (IL: 1/lambda_i of the POC elements)
-enum : int { KV_H, KV_Z, KV_S, KV_DZ, KV_DS, KV_RZ, KV_RS, KV_LAM, KV_WB, KV_CA, KV_CB, KV_K0,
-             KV_K1, KV_K2, KV_T1, KV_T2, KV_IL };
+// k-vector ids (IL: 1/lambda_i of the POC elements).  KV_RZ .. KV_T2 are
+// dead while a factorisation runs (the previous solve's results are consumed,
+// the next solve's temporaries not yet written): the Cholesky shapes' tile
+// transpose buffer lives there (Shape::O_TB).
+enum : int { KV_H, KV_Z, KV_S, KV_DZ, KV_DS, KV_LAM, KV_WB, KV_CA, KV_CB, KV_IL, KV_RZ, KV_RS, KV_K0,
+             KV_K1, KV_K2, KV_T1, KV_T2 };
+constexpr int NKV_DEAD = KV_T2 - KV_RZ + 1;
 
 template <int NQ, int NP, int MQ>
 struct Shape {
@@ -111,6 +119,8 @@ struct Shape {
   // reads may alias the next vector (the last one reads into the A block); every
   // write is guarded by i < k or the code, and rows [k, KP) stay zero.
   static constexpr int KS = KP;
+  static constexpr int O_RC = O_FIXED;       // rcode[KP]: cone*4 + type (0 POC, 1 SOC head, 2 SOC tail, 3 pad)
+  static constexpr int O_KV = O_RC + KP;     // 17 k-vectors, KS apart
   static constexpr int O_A = O_KV + NKV * KS;
   static constexpr int O_NV = O_A + MPAD * LDA;    // n-vectors: c x rd rx n0 tn
   static constexpr int O_MV = O_NV + 6 * NPAD;     // m-vectors: b y rp ry m0 tm
@@ -120,8 +130,11 @@ struct Shape {
   static constexpr int UAL = (AL_LDS && MPAD * LDA > NCS * NPAD) ? MPAD * LDA : NCS * NPAD;
   static constexpr int O_U = O_MV + 6 * MPAD;
   static constexpr int O_AL = O_U;
-  static constexpr int O_TB = O_U + UAL;           // tile transpose [16][17]
-  static constexpr int TOTAL = O_TB + 16 * 17;
+  // tile transpose [16][17]: only factor() uses it; on the Cholesky shapes
+  // (AL_LDS) in the k-vectors dead during a factorisation when they hold it
+  static constexpr bool TB_ALIAS = AL_LDS && NKV_DEAD * KS >= 16 * 17;
+  static constexpr int O_TB = TB_ALIAS ? O_KV + KV_RZ * KS : O_U + UAL;
+  static constexpr int TOTAL = O_U + UAL + (TB_ALIAS ? 0 : 16 * 17);
   static constexpr int nv(int id) { return O_NV + id * NPAD; }
   static constexpr int mv(int id) { return O_MV + id * MPAD; }
 };
@@ -140,7 +153,8 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
   int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = NPAD + 1;
   int KS = 4 * NP;  // Shape::KS
   int ual = (MQ == 1 && MPAD * LDA > NCS * NPAD) ? MPAD * LDA : NCS * NPAD;  // Shape::UAL
-  int total = O_KV + NKV * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + ual + 16 * 17;
+  const bool tb_alias = MQ == 1 && NKV_DEAD * KS >= 16 * 17;                // Shape::TB_ALIAS
+  int total = O_FIXED + KS + NKV * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + ual + (tb_alias ? 0 : 16 * 17);
   return (size_t)total * sizeof(double);
 }
 
@@ -469,6 +483,20 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
   e = fma(-(h * y), y, 0.5);
   return fma(y, e, y);
 }
+// the tile factorisation's pivots: SOCP_TILE_NEWTON Newton steps (1: a
+// shorter dependency chain, within a few ulp)
+#ifndef SOCP_TILE_NEWTON
+#define SOCP_TILE_NEWTON 1
+#endif
+__device__ __forceinline__ double rsqrt_tile(double d) {
+#if SOCP_TILE_NEWTON == 1
+  const double y = __builtin_amdgcn_rsq(d);
+  const double e = fma(-(0.5 * d) * y, y, 0.5);
+  return fma(y, e, y);
+#else
+  return rsqrt_nr(d);
+#endif
+}
 
 #ifndef SOCP_TILE_FACTOR
 #define SOCP_TILE_FACTOR 1
@@ -531,16 +559,16 @@ __device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok, cons
                    a13 = readlane_d(v, 16 + 4 * B + 3);
       const double a22 = readlane_d(v, 32 + 4 * B + 2), a23 = readlane_d(v, 32 + 4 * B + 3);
       const double a33 = readlane_d(v, 48 + 4 * B + 3);
-      const double rs0 = rsqrt_nr(a00);
+      const double rs0 = rsqrt_tile(a00);
       const double r01 = a01 * rs0, r02 = a02 * rs0, r03 = a03 * rs0;
       const double s11 = fma(-r01, r01, a11);
-      const double rs1 = rsqrt_nr(s11);
+      const double rs1 = rsqrt_tile(s11);
       const double r12 = fma(-r01, r02, a12) * rs1, r13 = fma(-r01, r03, a13) * rs1;
       const double s22 = fma(-r12, r12, fma(-r02, r02, a22));
-      const double rs2 = rsqrt_nr(s22);
+      const double rs2 = rsqrt_tile(s22);
       const double r23 = fma(-r12, r13, fma(-r02, r03, a23)) * rs2;
       const double s33 = fma(-r23, r23, fma(-r13, r13, fma(-r03, r03, a33)));
-      const double rs3 = rsqrt_nr(s33);
+      const double rs3 = rsqrt_tile(s33);
       ok = ok && (a00 > 0.0) && (s11 > 0.0) && (s22 > 0.0) && (s33 > 0.0);  // NaN fails too
       double V[4], X[4];
       row_bcast4(v, V);
@@ -589,7 +617,8 @@ struct Small {
   static constexpr int NT = NQ * (NQ + 1) / 2;
   static constexpr int MT = MQ * (MQ + 1) / 2;
   static constexpr int NPAD = SH::NPAD, KP = SH::KP, MPAD = SH::MPAD, LDA = SH::LDA;
-  static constexpr int O_A = SH::O_A, O_U = SH::O_U, O_AL = SH::O_AL, O_TB = SH::O_TB;
+  static constexpr int O_A = SH::O_A, O_U = SH::O_U, O_AL = SH::O_AL, O_TB = SH::O_TB, O_RC = SH::O_RC,
+                       O_KV = SH::O_KV;
   static constexpr bool AL_LDS = SH::AL_LDS;
   static constexpr int C_ = SH::nv(NV_C), X_ = SH::nv(NV_X), RD = SH::nv(NV_RD),
                        RX = SH::nv(NV_RX), N0 = SH::nv(NV_N0), TN = SH::nv(NV_TN);
@@ -644,7 +673,7 @@ struct Small {
       LDS(O_CDIM + lane) = a.cones.dim[lane];
       LDS(O_CKIND + lane) = a.cones.kind[lane];
     }
-    for (int i = lane; i < KMAX; i += 64) {
+    for (int i = lane; i < KP; i += 64) {
       int code = 3;
       if (i < k) {
         for (int c = 0; c < nc; ++c) {
@@ -660,7 +689,9 @@ struct Small {
     // segment partials: entry (v, c, slot) is written only when cone c meets the
     // slot, the same for every problem of the launch; the rest stays zero
     for (int e = lane; e < O_TOTC - O_PART; e += 64) LDS(O_PART + e) = 0.0;
+#ifdef SOCP_DIAG
     if (lane < 24) LDS(O_STAMPS + lane) = 0.0;  // all-zero bits: the u64 totals start at 0
+#endif
     SYNC();
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -725,7 +756,7 @@ struct Small {
 #pragma unroll
     for (int t = 0; t < AB; ++t) av[t] = (64 * t + lane < mn) ? Ap[64 * t + lane] : 0.0;
     for (int e = lane; e < NKV * SH::KS; e += 64) LDS(O_KV + e) = 0.0;
-    for (int e = lane; e < SH::O_TB - O_A; e += 64) LDS(O_A + e) = 0.0;
+    for (int e = lane; e < O_U + SH::UAL - O_A; e += 64) LDS(O_A + e) = 0.0;
     SYNC();
     if (lane < n) LDS(C_ + lane) = cv;
     if (lane < m) LDS(B_ + lane) = bv;
@@ -1662,6 +1693,16 @@ struct Small {
     return ok;
   }
 
+  // the transpose buffer, when it lives in dead k-vectors, is zeroed again at
+  // the end of a factorisation: their padding rows [k, KP) are never written
+  // by the solves and must read as zero (G'T2 reads them against G's zero rows)
+  __device__ __forceinline__ void clear_tb() {
+    if constexpr (SH::TB_ALIAS) {
+      SYNC();
+      for (int e = lane; e < 16 * 17; e += 64) LDS(O_TB + e) = 0.0;
+      SYNC();
+    }
+  }
   __device__ __forceinline__ d4 transpose(d4 t) {
     MARK_BEGIN("transpose");
     LANE_IDS();
@@ -1708,11 +1749,15 @@ struct Small {
     if constexpr (CHOL) {
       const bool okH = chol();
       STAMP(SP_SWEEP_H);
-      if (!okH) return ST_CHOL_H;
+      if (!okH) {
+        clear_tb();
+        return ST_CHOL_H;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (g + 4 * r == cl && cl >= m) Sv[0][r] = 1.0;
       const bool okS = sweep<1, false>(Sv);
+      clear_tb();
       STAMP(SP_SCHUR);
       if (!okS) return ST_CHOL_S;
       Sv[0] = -Sv[0];
@@ -1987,6 +2032,46 @@ struct Small {
     SYNC();
   }
 
+  // gemv_G and gemv_Gt in one pass over G (the residuals' Gx and G'z): each
+  // G element is copied out of its AGPRs once for both products; the
+  // accumulation orders are gemv_G's and gemv_Gt's, so the results are theirs
+  // bit for bit.  acc: lane partials of G'v (rows_sum'd by the caller).
+  template <int P0, int CH>
+  __device__ __forceinline__ void gemv_G2_chunk(const double (&uq)[NQ], double (&acc)[NQ], int v, int add1, int add2,
+                                                int out) {
+    LANE_IDS();
+    double P[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const double vp = LDS(v + 4 * (P0 + j) + g);
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const double gq = a_get(G[P0 + j][q]);
+        s = fma(gq, uq[q], s);
+        acc[q] = fma(gq, vp, acc[q]);
+      }
+      P[j] = s;
+    }
+    int base = 0;
+    rs16<CH, 8>(P, cl, base);
+    constexpr int CF = RSCount<CH, 8>::value;
+#pragma unroll
+    for (int j = 0; j < CF; ++j) {
+      const int row = 4 * (P0 + base + j) + g;
+      if (row < k) {
+        double w = P[j];
+        if (add1 >= 0) w = w + LDS(add1 + row);
+        w = w - LDS(add2 + row);
+        LDS(out + row) = w;
+      }
+    }
+    if constexpr (P0 + CH < NP) {
+      constexpr int NXT = (NP - P0 - CH) < 8 ? (NP - P0 - CH) : 8;
+      gemv_G2_chunk<P0 + CH, NXT>(uq, acc, v, add1, add2, out);
+    }
+  }
+
   // acc[q] (all lanes) = (G' v)[16q+cl]
   __device__ __forceinline__ void gemv_Gt(int v, double (&acc)[NQ]) {
     MARK_BEGIN("gemv_Gt");
@@ -2050,7 +2135,24 @@ struct Small {
     MARK_BEGIN("residuals");
     LANE_IDS();
     double acc[NQ], at[NQ];
+#ifndef SOCP_RESID_MERGE
+#define SOCP_RESID_MERGE 0
+#endif
+#if SOCP_RESID_MERGE
+    {  // G'z and Gx + s - h in one pass over G
+      double uq[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        uq[q] = LDS(X_ + 16 * q + cl);
+        acc[q] = 0.0;
+      }
+      gemv_G2_chunk<0, (NP < 8 ? NP : 8)>(uq, acc, Z_, S_, H_, DZ);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[q] = rows_sum(acc[q]);
+    }
+#else
     gemv_Gt(Z_, acc);
+#endif
     At_mv(Y_, at);
     double d2 = 0.0, zs = 0.0;
     if (g == 0) {
@@ -2065,7 +2167,11 @@ struct Small {
       }
     }
     const double p2 = A_mv(X_, B_, RP);
+#if SOCP_RESID_MERGE
+    SYNC();
+#else
     gemv_G(X_, S_, H_, DZ);
+#endif
     for (int i = lane; i < k; i += 64) zs += LDS(Z_ + i) * LDS(S_ + i);
     nd = sqrt(wsum(d2));
     np_ = sqrt(wsum(p2));
