@@ -26,7 +26,8 @@ constexpr int LARGE_NB_MAX = 8;  // NPAD, MPAD <= 512: a swept panel row lives i
 struct LargeLayout {
   int NPAD, MPAD, KP, RW;  // n, m rounded up to 64, k to 16; RW = max(NPAD, MPAD)
   // LDS offsets (doubles)
-  int o_rc, o_cc, o_kv, o_nv, o_mv, o_row, o_rv, o_part, o_red, o_fx, total;
+  int o_rc, o_cc, o_kvd, o_kvl, o_nv, o_mv, o_row, o_rv, o_part, o_red, o_fx, total;
+  int sy;  // 1: the staged SYRK's four chunk buffers fit (socp_large.hip form_H_staged_g)
   // workspace-slot offsets (doubles)
   int64_t w_x, w_h, w_ap, w_at, w_yp, w_rv, w_t, w_s, w_v, w_total;
   // per-problem factor record (socp_dense handles): what solve_kkt reads
@@ -39,18 +40,30 @@ __host__ __device__ inline LargeLayout large_layout(int n, int m, int k) {
   L.MPAD = ((m > 0 ? m : 1) + 63) / 64 * 64;
   L.KP = (k + 15) / 16 * 16;
   L.RW = L.NPAD > L.MPAD ? L.NPAD : L.MPAD;
-  int o = 0;
-  L.o_rc = o;   o += L.KP;          // element code: cone*4 + type
-  L.o_cc = o;   o += 12 * MAXC;     // per-cone constants CC_*
-  L.o_kv = o;   o += 15 * L.KP;     // k-vectors
-  L.o_nv = o;   o += 6 * L.NPAD;    // n-vectors
-  L.o_mv = o;   o += 5 * L.MPAD;    // m-vectors
-  L.o_row = o;  o += 2 * L.RW > 1024 ? 2 * L.RW : 1024;  // sweep: pivot rows / four 16x16 tile slots
-  L.o_rv = o;   o += 64;            // sweep: -1/d of the panel's pivots
-  L.o_part = o; o += 8 * L.MPAD;    // A x partial sums per wavefront
-  L.o_red = o;  o += 64;            // block reductions
-  L.o_fx = o;   o += 8 * 64;        // W^-1 G fast path: per wavefront, per-cone sums and heads
-  L.total = o;
+  // The region from 0 holds what is dead while a factorisation runs -- seven
+  // k-vectors (RZ RS K0 K1 K2 T1 T2) and the sweep / solve scratch -- so the
+  // staged SYRK's four 4-row X chunk buffers (4 NPAD doubles each, written by
+  // LDS-DMA, whose destination must lie in the first 64 KiB) can overlay it,
+  // padded up to 16 NPAD when NPAD is 256 or 512 and the LDS allows.
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool want = pass == 0 && (L.NPAD == 256 || L.NPAD == 512);
+    int o = 0;
+    L.o_kvd = o;  o += 7 * L.KP;      // dead k-vectors
+    L.o_row = o;  o += 2 * L.RW > 1024 ? 2 * L.RW : 1024;  // sweep: pivot rows / four 16x16 tile slots
+    L.o_rv = o;   o += 64;            // sweep: -1/d of the panel's pivots
+    L.o_part = o; o += 8 * L.MPAD;    // A x partial sums per wavefront
+    if (want && o < 16 * L.NPAD) o = 16 * L.NPAD;
+    L.o_kvl = o;  o += 8 * L.KP;      // live k-vectors (H Z S DZ DS LAM WB CA)
+    L.o_rc = o;   o += L.KP;          // element code: cone*4 + type
+    L.o_cc = o;   o += 12 * MAXC;     // per-cone constants CC_*
+    L.o_nv = o;   o += 6 * L.NPAD;    // n-vectors
+    L.o_mv = o;   o += 5 * L.MPAD;    // m-vectors
+    L.o_red = o;  o += 64;            // block reductions (slot 63: the next problem index)
+    L.o_fx = o;   o += 8 * 64;        // W^-1 G fast path: per wavefront, per-cone sums and heads
+    L.total = o;
+    L.sy = want ? 1 : 0;
+    if (!want || (long)o * 8 + 64 <= 160 * 1024) break;
+  }
   int64_t w = 0;
   L.w_x = w;  w += large_al((int64_t)L.KP * L.NPAD);    // X = W^-1 G
   L.w_h = w;  w += large_al((int64_t)L.NPAD * L.NPAD);  // H -> Li

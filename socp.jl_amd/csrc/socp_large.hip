@@ -137,22 +137,23 @@ struct Large {
         wv(__builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6)), ws0((gdbl*)la.ws), rec0((gdbl*)la.rec),
         wstride(la.wstride) {
     set_slot(blockIdx.x);
-    const int kv = L.o_kv, KP = L.KP;
-    H_ = kv;
-    Z_ = kv + KP;
-    S_ = kv + 2 * KP;
-    DZ = kv + 3 * KP;
-    DS = kv + 4 * KP;
-    RZ = kv + 5 * KP;
-    RS = kv + 6 * KP;
-    LAM = kv + 7 * KP;
-    WB = kv + 8 * KP;
-    CA = kv + 9 * KP;
-    K0 = kv + 10 * KP;
-    K1 = kv + 11 * KP;
-    K2 = kv + 12 * KP;
-    T1 = kv + 13 * KP;
-    T2 = kv + 14 * KP;
+    const int kl = L.o_kvl, kd = L.o_kvd, KP = L.KP;
+    H_ = kl;
+    Z_ = kl + KP;
+    S_ = kl + 2 * KP;
+    DZ = kl + 3 * KP;
+    DS = kl + 4 * KP;
+    LAM = kl + 5 * KP;
+    WB = kl + 6 * KP;
+    CA = kl + 7 * KP;
+    // dead while a factorisation runs (under the staged SYRK's buffers)
+    RZ = kd;
+    RS = kd + KP;
+    K0 = kd + 2 * KP;
+    K1 = kd + 3 * KP;
+    K2 = kd + 4 * KP;
+    T1 = kd + 5 * KP;
+    T2 = kd + 6 * KP;
     const int nv = L.o_nv, NP = L.NPAD;
     C_ = nv;
     X_ = nv + NP;
@@ -286,7 +287,9 @@ struct Large {
 
   __device__ void load(int64_t p) {
     Gp = (gcdbl*)a.G + p * (int64_t)k * n;
-    for (int e = tid; e < 15 * L.KP + 6 * L.NPAD + 5 * L.MPAD; e += NTH) LV(L.o_kv + e) = 0.0;
+    for (int e = tid; e < 7 * L.KP; e += NTH) LV(L.o_kvd + e) = 0.0;
+    for (int e = tid; e < 8 * L.KP; e += NTH) LV(L.o_kvl + e) = 0.0;
+    for (int e = tid; e < 6 * L.NPAD + 5 * L.MPAD; e += NTH) LV(L.o_nv + e) = 0.0;
     BAR();
     for (int j = tid; j < n; j += NTH) LV(C_ + j) = a.c[p * n + j];
     for (int i = tid; i < m; i += NTH) LV(B_ + i) = a.b[p * m + i];
@@ -765,10 +768,14 @@ struct Large {
   // round trip per pass), reduces every cone's wbar-weighted tail sum from
   // registers, and writes the columns of X.  Otherwise form_X.
   static constexpr int FX_CG = 4, FX_NC = 8, FX_R = 10;
-  __device__ bool form_X_fast() {
+  __device__ bool form_X_fast_ok() const { return nc - csoc <= FX_NC && (k + 63) / 64 <= FX_R; }
+  // chunked: X in 4-row chunks, chunk-major -- X[i][j] at ((i/4) NPAD + j) 4 + i%4
+  // -- so a chunk is one contiguous 32 NPAD-byte run (the staged SYRK's DMA)
+  __device__ bool form_X_fast(bool chunked) {
     const int nsoc = nc - csoc;
     const int R = (k + 63) / 64;
-    if (nsoc > FX_NC || R > FX_R) return false;
+    if (!form_X_fast_ok()) return false;
+    const int NPD = L.NPAD;
     const int KP = L.KP, ln = lane, kk = k, nn = n;
     const int fx = L.o_fx + wv * 64;  // [0,32): del[u][c], [32,64): head value g0[u][c]
     for (int j0 = FX_CG * wv; j0 < L.NPAD; j0 += FX_CG * NW) {
@@ -830,7 +837,12 @@ struct Large {
           if (typ == 1) x = im * (wb0 * g - del);
           if (typ == 2) x = im * (g + (-gh + del * i1) * wbr[r]);
           if (u >= nl) x = 0.0;
-          if (row < KP) x0[u * KP + row] = x;
+          if (row < KP) {
+            if (chunked)
+              Xw[((int64_t)(row >> 2) * NPD + j0 + u) * 4 + (row & 3)] = x;
+            else
+              x0[u * KP + row] = x;
+          }
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -886,6 +898,157 @@ struct Large {
       }
     }
     BAR();
+  }
+
+  // ------------------------------------------------ staged SYRK (LDS-DMA)
+  // H = X'X with X streamed through LDS in 4-row chunks (all NPAD columns,
+  // 32 contiguous bytes per column), shared by the eight wavefronts: each
+  // wavefront accumulates one 64x64 block per pass over X (ceil(blocks / 8)
+  // passes), so X is read once per pass instead of two 64-column panels per
+  // block.  The chunks land in LDS by global_load_lds_dwordx4 (no VGPRs: the
+  // kernel is at the 256-VGPR cap of 8 waves per CU), three chunks in flight
+  // in a ring of four buffers; one LDS barrier per chunk, preceded by a
+  // counted vmcnt that retires this wave's DMA of the chunk about to be read
+  // (its DMAs of the two younger chunks stay in flight).  The asm DMAs are
+  // outside hipcc's wait bookkeeping; extra in-flight ops only strengthen the
+  // waits it emits for its own loads.
+#ifndef SOCP_LG_STAGED
+#define SOCP_LG_STAGED 0  // A/B: 1 = the LDS-DMA staged SYRK
+#endif
+  // a 64-bit pointer made wave-uniform (SGPRs): __builtin_amdgcn_readfirstlane
+  // takes and returns int, so the halves go separately
+  __device__ __forceinline__ static gcdbl* uni_ptr(gcdbl* p) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return (gcdbl*)(((unsigned long long)hi << 32) | lo);
+  }
+  template <int N>
+  __device__ __forceinline__ static void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  }
+  // this wave's DMA of chunk c: column groups cg = w + 8t (t < GPW) of 32
+  // columns; lane L copies rows 4c + 2(L & 1) .. +1 of column 32 cg + L/2 to
+  // byte 1024 cg + 16 L of the buffer (lane-linear)
+  // (saddr form: X's base in SGPRs, a 32-bit per-lane byte offset)
+  // base: the chunk's first row of column 0 (wave-uniform); voff[t]: the
+  // lane's byte offset from it (loop-invariant)
+  template <int GPW>
+  __device__ __forceinline__ static void glds_chunk(gcdbl* base, const unsigned (&voff)[GPW], unsigned bufb, int w) {
+#pragma unroll
+    for (int t = 0; t < GPW; ++t) {
+      const unsigned dst = __builtin_amdgcn_readfirstlane(bufb + 1024u * (unsigned)(w + 8 * t));
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(voff[t]), "s"(base), "s"(dst)
+          : "memory");
+    }
+  }
+  // noinline: its own register allocation (the kernel body is at the 256-VGPR
+  // cap and spills; a scratch reload inside the chunk loop would wait for every
+  // DMA in flight)
+  template <int GPW>
+  __device__ __attribute__((noinline)) void form_H_staged_g(bool addAA) {
+#define UNI(x) __builtin_amdgcn_readfirstlane(x)
+    const int NP = UNI(L.NPAD), KP = UNI(L.KP), NB = NP / 64, nblk = NB * (NB + 1) / 2, NCH = KP / 4;
+    const int w_ = UNI(wv), b0 = UNI(L.o_kvd);
+#undef UNI
+    const int ln = lane, g = lane >> 4, cl = lane & 15;
+    gcdbl* const xw = uni_ptr((gcdbl*)Xw);
+    // buffer q: LDS double offset and byte address (arithmetic, not a local
+    // array: a dynamically indexed array would live in scratch)
+    const int CS = 4 * NP;
+    const unsigned lbase = (unsigned)(uintptr_t)((__attribute__((address_space(3))) double*)lg_lds);
+    auto boff = [&](int q) { return b0 + q * CS; };
+    auto bbyte = [&](int q) { return lbase + 8u * (unsigned)boff(q); };
+    // A'A (sing) rides along as the rows of A after those of X: [X; A]'[X; A]
+    gcdbl* const ap = uni_ptr((gcdbl*)Ap);
+    const int MP = __builtin_amdgcn_readfirstlane(L.MPAD);
+    const int NCT = __builtin_amdgcn_readfirstlane(NCH + (addAA ? MP / 4 : 0));
+    // lane L of column group cg copies 16 bytes: column 32 cg + L/2, rows 2(L & 1) .. +1
+    // X is chunk-major (form_X_fast(chunked)): a wave-instruction copies 1 KiB
+    // of contiguous bytes; A (column-major, leading dimension MPAD) 32 bytes per column
+    unsigned vx[GPW], va[GPW];
+#pragma unroll
+    for (int t = 0; t < GPW; ++t) {
+      const int col = 32 * (w_ + 8 * t) + (ln >> 1);
+      vx[t] = (unsigned)((128 * (w_ + 8 * t) + 2 * ln) * 8);
+      va[t] = (unsigned)((col * MP + 2 * (ln & 1)) * 8);
+    }
+    auto issue = [&](int c) {
+      if (c < NCH)
+        glds_chunk<GPW>(xw + (int64_t)4 * NP * c, vx, bbyte(c & 3), w_);
+      else
+        glds_chunk<GPW>(ap + 4 * (c - NCH), va, bbyte(c & 3), w_);
+    };
+    for (int pass = 0; pass * NW < nblk; ++pass) {
+      const int b = pass * NW + w_;
+      const bool act = b < nblk;
+      int I = 0, J = 0;
+      if (act) tri_ij(b, I, J);
+      I = __builtin_amdgcn_readfirstlane(I);
+      J = __builtin_amdgcn_readfirstlane(J);
+      const bool dg = I == J;
+      d4 acc[4][4];
+      zero_blk(acc);
+      // vmcnt(0) as the builtin (hipcc tracks it): the previous pass's block
+      // stores retire here, not in every chunk step (with them pending at the
+      // loop head, hipcc waits vmcnt(0) before each step's LDS reads, which
+      // would also drain the DMA ring)
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (q < NCT) issue(q);
+      for (int c = 0; c < NCT; ++c) {
+        const int ahead = NCT - 1 - c;  // chunks issued after c (at most 2 at this point)
+        if (ahead >= 2)
+          wait_vm<2 * GPW>();
+        else if (ahead == 1)
+          wait_vm<GPW>();
+        else
+          wait_vm<0>();
+        LDS_BAR();
+        if (c + 3 < NCT) issue(c + 3);
+        if (act) {  // all 16 tiles, also on a diagonal block (one code path: a
+                    // branch between tile sets costs register copies of acc)
+          const int buf = boff(c & 3);
+          double av[4], bv[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            av[t] = LV(buf + (64 * I + 16 * t + cl) * 4 + g);
+            bv[t] = LV(buf + (64 * J + 16 * t + cl) * 4 + g);
+          }
+#pragma unroll
+          for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+            for (int tb = 0; tb < 4; ++tb) acc[ta][tb] = mfma(av[ta], bv[tb], acc[ta][tb]);
+        }
+      }
+      if (act) {
+        if (dg)
+          store_blk<true>(acc, Hm, NP, 64 * I, 64 * J, n);
+        else
+          store_blk(acc, Hm, NP, 64 * I, 64 * J, n);
+      }
+      LDS_BAR();  // every read of this pass done before the next pass restages
+    }
+    // the buffers overlay the dead k-vectors: zero them again (their padding
+    // rows must read 0)
+    for (int e = tid; e < 7 * KP; e += NTH) LV(b0 + e) = 0.0;
+    BAR();
+  }
+  // the LDS-DMA destination (M0) kept inside the first 64 KiB
+  __device__ bool staged_ok() const {
+    const unsigned lbase = (unsigned)(uintptr_t)((__attribute__((address_space(3))) double*)(lg_lds + L.o_kvd));
+    return SOCP_LG_STAGED && L.sy && lbase + 128u * (unsigned)L.NPAD <= 65536u;
+  }
+  __device__ void form_H_staged(bool addAA) {
+    if (L.NPAD == 512)
+      form_H_staged_g<2>(addAA);
+    else
+      form_H_staged_g<1>(addAA);
   }
 
   // H = X'X (+A'A) (densesolver.jl:42-46): lower 64x64 blocks, one wavefront
@@ -1437,9 +1600,13 @@ struct Large {
   // setup_iter (densesolver.jl:41-52): H (+A'A), Li = H^-1, T = Li A', S = A T, S^-1
   __device__ int factor(bool addAA, bool h_only) {
     LSTAMP(SP_OTHER);
-    if (!form_X_fast()) form_X();
+    const bool stg = form_X_fast_ok() && staged_ok();
+    if (!form_X_fast(stg)) form_X();
     LSTAMP(SP_U);
-    form_H(addAA);
+    if (stg)
+      form_H_staged(addAA);
+    else
+      form_H(addAA);
     LSTAMP(SP_SYRK);
 #if SOCP_LG_CHOL
     if (!chol(Hm, L.NPAD)) return ST_CHOL_H;
@@ -1955,13 +2122,16 @@ struct Large {
 };
 
 __global__ void __launch_bounds__(NTH, 1) socp_large_kernel(LargeArgs args) {
-  __shared__ int pidx;
+  // the next problem index lives in dynamic LDS (slot 63 of the block-reduction
+  // area): no static LDS, so lg_lds starts at LDS address 0 and the staged
+  // SYRK's DMA buffers lie in the first 64 KiB
   Large S(args);
   S.init_tables();
+  const int pslot = S.L.o_red + 63;
   while (true) {
-    if (threadIdx.x == 0) pidx = atomicAdd(args.a.counter, 1);
+    if (threadIdx.x == 0) LV(pslot) = (double)atomicAdd(args.a.counter, 1);
     __syncthreads();
-    const int64_t p = pidx;
+    const int64_t p = (int64_t)LV(pslot);
     __syncthreads();  // everyone has read pidx before thread 0 overwrites it
     if (p >= args.a.B) break;
     S.run(p);

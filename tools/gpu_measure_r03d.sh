@@ -5,8 +5,10 @@
 # phase stamps (diagnostic library).  Phase 2 (tools/gpu_bench_r03.sh) runs the
 # bench lines against the committed profiles/r03_* traffic files.
 set -e
+timeout -k 10 120 ./tools/probe_tile > gpurun_out/r03d_probe_tile.log 2>&1 || { cat gpurun_out/r03d_probe_tile.log; exit 1; }
+cat gpurun_out/r03d_probe_tile.log
 export TMPDIR=/tmp
-O=gpurun_out/r03c
+O=gpurun_out/r03d
 mkdir -p $O
 pmc() {  # name config batch K extra-args
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f_$1 -o f -- python3 bench.py --config $2 --steps 1 --warmup 0 --no-cpu --no-ingest > $O/pmc_f_$1.log 2>&1 || { tail -20 $O/pmc_f_$1.log; exit 1; }
