@@ -1711,6 +1711,73 @@ struct Large {
     BAR();
     LSTAMP(NSTAMP + 1 + 5);
   }
+  // The residuals' two G products in one pass over G (solver.jl:110-118):
+  // vout = G'zin and gout[i] = (G xin)[i] + add[i] - sub[i].  As gemv_Gt's fast
+  // path, a wavefront holds CGM columns whole; it also accumulates its lanes'
+  // rows' share of G xin over its columns, and the eight per-wave partial
+  // vectors meet in the LDS region that is dead outside a solve (the seven
+  // dead k-vectors and the sweep scratch, from 0), summed in wave order.
+  // Returns false (the two separate passes run instead) where the shape
+  // does not fit that.
+  static constexpr int CGM = 4;
+  __device__ bool gemv_GtG(int zin, int vout, int xin, int add, int sub, int gout) {
+    const int KP = L.KP;
+    if (!SOCP_LG_GT_FAST || k > 64 * GT_R || L.o_kvd != 0 || 8 * KP > L.o_part + 8 * L.MPAD) return false;
+    LSTAMP(SP_SOLVE);
+    double vr[GT_R], pr[GT_R];
+#pragma unroll
+    for (int r = 0; r < GT_R; ++r) {
+      vr[r] = (lane + 64 * r < k) ? LV(zin + lane + 64 * r) : 0.0;
+      pr[r] = 0.0;
+    }
+    for (int j0 = CGM * wv; j0 < n; j0 += CGM * NW) {
+      gcdbl* g0 = Gp + (int64_t)j0 * k;
+      const int nl = n - j0;
+      double gv[CGM][GT_R], xs[CGM];
+#pragma unroll
+      for (int u = 0; u < CGM; ++u) {
+        xs[u] = u < nl ? LV(xin + j0 + u) : 0.0;
+#pragma unroll
+        for (int r = 0; r < GT_R; ++r) {
+          const int row = lane + 64 * r;
+          gv[u][r] = (row < k) ? g0[(int64_t)(u < nl ? u : 0) * k + row] : 0.0;
+        }
+      }
+      double acc[CGM];
+#pragma unroll
+      for (int u = 0; u < CGM; ++u) {
+        acc[u] = 0.0;
+#pragma unroll
+        for (int r = 0; r < GT_R; ++r) acc[u] = fma(gv[u][r], vr[r], acc[u]);
+      }
+#pragma unroll
+      for (int r = 0; r < GT_R; ++r)
+#pragma unroll
+        for (int u = 0; u < CGM; ++u) pr[r] = fma(gv[u][r], xs[u], pr[r]);
+#pragma unroll
+      for (int u = 0; u < CGM; ++u) {
+        const double sm = wave_sum(acc[u]);
+        if (lane == 0 && j0 + u < n) LV(vout + j0 + u) = sm;
+      }
+    }
+    const int part = L.o_kvd;
+#pragma unroll
+    for (int r = 0; r < GT_R; ++r)
+      if (lane + 64 * r < KP) LV(part + wv * KP + lane + 64 * r) = pr[r];
+    BAR();
+    for (int i = tid; i < k; i += NTH) {
+      double sm = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sm += LV(part + w * KP + i);
+      if (add >= 0) sm = sm + LV(add + i);
+      LV(gout + i) = sm - LV(sub + i);
+    }
+    BAR();
+    for (int e = tid; e < 7 * KP; e += NTH) LV(part + e) = 0.0;  // the dead k-vectors read 0 again
+    BAR();
+    LSTAMP(NSTAMP + 1 + 5);
+    return true;
+  }
   // out[i] = (G u)[i] (+ add[i]) - sub[i] for i < k: one thread per row
   __device__ void gemv_G(int u, int add, int sub, int out) {
     LSTAMP(SP_SOLVE);
@@ -1846,7 +1913,8 @@ struct Large {
 
   // rd = A'y + G'z + c, rp = Ax - b, rz = Gx + s - h (solver.jl:109-118)
   __device__ void residuals(double& nd, double& np_, double& gap) {
-    gemv_Gt(Z_, TN, -1);
+    const bool merged = gemv_GtG(Z_, TN, X_, S_, H_, DZ);  // G'z and Gx + s - h in one G pass
+    if (!merged) gemv_Gt(Z_, TN, -1);
     double d2 = 0.0;
     for (int j = tid; j < n; j += NTH) {
       const double v = (At_dot(Y_, j) + LV(TN + j)) + LV(C_ + j);
@@ -1854,7 +1922,7 @@ struct Large {
       d2 = fma(v, v, d2);
     }
     const double p2 = A_mv(X_, B_, RP);
-    gemv_G(X_, S_, H_, DZ);
+    if (!merged) gemv_G(X_, S_, H_, DZ);
     double zs = 0.0;
     for (int i = tid; i < k; i += NTH) zs += LV(Z_ + i) * LV(S_ + i);
     nd = sqrt(block_sum(d2));
