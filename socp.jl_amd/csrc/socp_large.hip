@@ -1778,15 +1778,40 @@ struct Large {
     LSTAMP(NSTAMP + 1 + 5);
     return true;
   }
-  // out[i] = (G u)[i] (+ add[i]) - sub[i] for i < k: one thread per row
+  // out[i] = (G u)[i] (+ add[i]) - sub[i] for i < k: one thread per row.  When
+  // NTH < k <= 2 NTH the rows past the first NTH are split over T = NTH/(k-NTH)
+  // threads of one wavefront each (column slices, a shuffle sum), so the second
+  // round costs 1/T of the first instead of a whole one with most threads idle.
   __device__ void gemv_G(int u, int add, int sub, int out) {
     LSTAMP(SP_SOLVE);
-    for (int i = tid; i < k; i += NTH) {
+    const int r2 = k - NTH;
+    int T = 0;
+    if (r2 > 0 && r2 <= NTH) {
+      T = 1;
+      while (T < 64 && T * 2 * r2 <= NTH) T *= 2;
+    }
+    const int i1 = T > 1 ? (k < NTH ? k : NTH) : k;  // rows done one thread each
+    for (int i = tid; i < i1; i += NTH) {
       double acc = 0.0;
 #pragma unroll 16
       for (int j = 0; j < n; ++j) acc = fma(Gp[(int64_t)j * k + i], LV(u + j), acc);
       if (add >= 0) acc = acc + LV(add + i);
       LV(out + i) = acc - LV(sub + i);
+    }
+    if (T > 1) {
+      const int i = NTH + tid / T, q = tid % T;  // T | 64: a row's threads share a wavefront
+      const int js = (n + T - 1) / T, j0 = q * js, j1 = j0 + js < n ? j0 + js : n;
+      const bool live = i < k;
+      double acc = 0.0;
+      if (live) {
+#pragma unroll 8
+        for (int j = j0; j < j1; ++j) acc = fma(Gp[(int64_t)j * k + i], LV(u + j), acc);
+      }
+      for (int d = 1; d < T; d *= 2) acc += __shfl_xor(acc, d, 64);
+      if (live && q == 0) {
+        if (add >= 0) acc = acc + LV(add + i);
+        LV(out + i) = acc - LV(sub + i);
+      }
     }
     BAR();
     LSTAMP(NSTAMP + 1 + 7);
