@@ -504,6 +504,9 @@ __device__ __forceinline__ double rsqrt_tile(double d) {
 #ifndef SOCP_TRANSPOSE_MFMA
 #define SOCP_TRANSPOSE_MFMA 0
 #endif
+#ifndef SOCP_TILE_INPLACE
+#define SOCP_TILE_INPLACE 1  // 0: copy back only registers > B (A/B builds)
+#endif
 #if SOCP_TILE_FACTOR == 0
 // Pivot J of row block B of the tile factorisation: v = register B of the
 // (updated) D tile, w = register B of the eliminated identity.  Row J of
@@ -537,7 +540,7 @@ struct NoHook {
   template <int B>
   __device__ __forceinline__ void run() const {}
 };
-template <int B, class H = NoHook>
+template <int B, bool INPL = (SOCP_TILE_INPLACE != 0), class H = NoHook>
 __device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok, const H& hook = H()) {
   if constexpr (B < 4) {
     LANE_IDS();
@@ -587,7 +590,12 @@ __device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok, cons
 #endif
     hook.template run<B>();  // independent MFMA work interleaved with the chain
     W[B] = Wb;
-    if constexpr (B < 3) {
+    if constexpr (B < 3 && INPL) {
+      // whole tiles: registers <= B are never read again (the later blocks read
+      // registers B+1..3), so the MFMA results replace Dt and It in place
+      Dt = __builtin_amdgcn_mfma_f64_16x16x4f64(R, R, Dt, 0, 0, 1);   // Dt -= R'R
+      It = __builtin_amdgcn_mfma_f64_16x16x4f64(R, Wb, It, 0, 0, 1);  // It -= R'W
+    } else if constexpr (B < 3) {
       const d4 t = __builtin_amdgcn_mfma_f64_16x16x4f64(R, R, Dt, 0, 0, 1);   // Dt -= R'R
       const d4 u = __builtin_amdgcn_mfma_f64_16x16x4f64(R, Wb, It, 0, 0, 1);  // It -= R'W
 #pragma unroll
@@ -596,10 +604,14 @@ __device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok, cons
         It[r] = u[r];
       }
     }
-    tile_block<B + 1>(Dt, It, W, ok, hook);
+    tile_block<B + 1, INPL>(Dt, It, W, ok, hook);
   }
 }
-template <class H = NoHook>
+// INPL: the trailing updates replace the tiles whole (one factorisation 3,126
+// cycles vs 3,406 on one wave, profiles/r03_probe_tile.log); the copying form
+// keeps fewer registers live, which the smallest register kernels need to stay
+// at two waves per SIMD.
+template <bool INPL = (SOCP_TILE_INPLACE != 0), class H = NoHook>
 __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok, const H& hook = H()) {
   MARK_BEGIN("factor_tile");
   LANE_IDS();
@@ -607,7 +619,7 @@ __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok, const H& hoo
 #pragma unroll
   for (int r = 0; r < 4; ++r) It[r] = (g + 4 * r == cl) ? 1.0 : 0.0;
   W = It;
-  tile_block<0>(Dt, It, W, ok, hook);
+  tile_block<0, INPL>(Dt, It, W, ok, hook);
 }
 
 
@@ -620,6 +632,10 @@ struct Small {
   static constexpr int O_A = SH::O_A, O_U = SH::O_U, O_AL = SH::O_AL, O_TB = SH::O_TB, O_RC = SH::O_RC,
                        O_KV = SH::O_KV;
   static constexpr bool AL_LDS = SH::AL_LDS;
+  // in-place tile updates (factor_tile) except where G is small enough for two
+  // waves per SIMD: C1's <2, 12, 1> takes 209 + 48 registers with them, 208 + 48
+  // without
+  static constexpr bool TILE_INPL = SOCP_TILE_INPLACE != 0 && NQ * NP > 24;
   static constexpr int C_ = SH::nv(NV_C), X_ = SH::nv(NV_X), RD = SH::nv(NV_RD),
                        RX = SH::nv(NV_RX), N0 = SH::nv(NV_N0), TN = SH::nv(NV_TN);
   static constexpr int B_ = SH::mv(MV_B), Y_ = SH::mv(MV_Y), RP = SH::mv(MV_RP),
@@ -1547,10 +1563,10 @@ struct Small {
         M[tri(P + 1, P + 1)] = mm<1>(Y[P + 1], Y[P + 1], M[tri(P + 1, P + 1)]);
         d4 Wn;
 #if SOCP_SWEEP_LOOKAHEAD
-        factor_tile(M[tri(P + 1, P + 1)], Wn, ok, PanelHook<Q, P>{M, Y, W});
+        factor_tile<TILE_INPL>(M[tri(P + 1, P + 1)], Wn, ok, PanelHook<Q, P>{M, Y, W});
 #else
         do_panel_ops<Q, P, 0, panel_op_count<Q, P>()>(M, Y, W);
-        factor_tile(M[tri(P + 1, P + 1)], Wn, ok);
+        factor_tile<TILE_INPL>(M[tri(P + 1, P + 1)], Wn, ok);
 #endif
         STAMP_SUB(1);
         sweep_panel<Q, SUBST, P + 1>(M, Id, Wn, ok);
@@ -1563,7 +1579,7 @@ struct Small {
   template <int Q, bool SUBST>
   __device__ __forceinline__ void sweep_tiles(d4 (&M)[Q * (Q + 1) / 2], const d4& Id, bool& ok) {
     d4 W;
-    factor_tile(M[tri(0, 0)], W, ok);
+    factor_tile<TILE_INPL>(M[tri(0, 0)], W, ok);
     STAMP_SUB(0);
     sweep_panel<Q, SUBST, 0>(M, Id, W, ok);
   }
@@ -1674,7 +1690,7 @@ struct Small {
         T[tri(P + 1, P)] = mm<0>(WT, T[tri(P + 1, P)], (d4){0.0, 0.0, 0.0, 0.0});
         T[tri(P + 1, P + 1)] = mm<1>(T[tri(P + 1, P)], T[tri(P + 1, P)], T[tri(P + 1, P + 1)]);
         d4 Wn;
-        factor_tile(T[tri(P + 1, P + 1)], Wn, ok, CholHook<P>{*this, WT});
+        factor_tile<TILE_INPL>(T[tri(P + 1, P + 1)], Wn, ok, CholHook<P>{*this, WT});
         T[tri(P, P)] = W;
         chol_panel<P + 1>(Wn, ok);
       } else {
@@ -1687,7 +1703,7 @@ struct Small {
     Sv[0] = (d4){0.0, 0.0, 0.0, 0.0};
     bool ok = true;
     d4 W;
-    factor_tile(T[tri(0, 0)], W, ok);
+    factor_tile<TILE_INPL>(T[tri(0, 0)], W, ok);
     chol_panel<0>(W, ok);
     SYNC();
     return ok;
