@@ -20,3 +20,5 @@ timeout -k 10 400 python3 bench.py --config C4 --steps 3 --warmup 1 --no-ingest 
 tail -1 $O/bench_c4.log | cut -c1-300
 timeout -k 10 300 python3 bench.py --config C1 --no-ingest > $O/bench_c1.log 2>&1 || { tail -30 $O/bench_c1.log; exit 1; }
 tail -1 $O/bench_c1.log | cut -c1-300
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4 -o c4 -- python3 bench.py --config C4 --steps 3 --warmup 1 --no-cpu --no-ingest > $O/prof_c4.log 2>&1 || { tail -30 $O/prof_c4.log; exit 1; }
+grep socp_large $O/prof_c4/c4_kernel_stats.csv | cut -c1-150
