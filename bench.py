@@ -40,6 +40,20 @@ def flops_per_problem_iter(n, m, k, sing=False):
             + 16 * k * n + 12 * m * n + 4 * n * n + 4 * m * m + (n * n if sing else 0))
 
 
+def flops_executed_per_problem_iter(n, m, k, sing=False, large=False):
+    """FP64 work the kernels actually execute per problem-iteration.  Where
+    H = L L' is factored and Li is never formed (the register kernel for
+    m <= 16, densesolver.jl:47 cholesky! + triangular solves; the blocked
+    kernel's default SOCP_LG_CHOL build) potrf is n^3/3 and Z = L^-1 A' is
+    m n^2, in place of potrf + potri (n^3) and A*Li (2 m n^2) of the SURVEY.md
+    §8(d) formula; the Gauss-Jordan sweep path (register kernel, m > 16) forms
+    Li and executes the formula's figure."""
+    if not (large or m <= 16):
+        return flops_per_problem_iter(n, m, k, sing)
+    return (n * (n + 1) * k + n ** 3 / 3.0 + m * n * n + m * (m + 1) * n + m ** 3 / 3.0
+            + 16 * k * n + 12 * m * n + 4 * n * n + 4 * m * m + (n * n if sing else 0))
+
+
 def bytes_per_problem_iter(n, m, k):
     """G, A read once; c, b, h; x, y, z, s read + write."""
     return 8 * (k * n + m * n) + 8 * (n + m + k) + 16 * (n + m + 2 * k)
@@ -417,6 +431,8 @@ def main():
         kms = sum(kernel_ms) / len(kernel_ms)
         iters_per_launch = int(out["iters"].sum().item())
         F = flops_per_problem_iter(n, m, k)
+        kname = ctx.last_kernel_name()
+        Fx = flops_executed_per_problem_iter(n, m, k, large="large" in kname)
         Bq = bytes_per_problem_iter(n, m, k)
         # binding bound of the algorithmic model: FP64 when F/B is above the
         # ridge (C2, C4), HBM below it (C1)
@@ -456,7 +472,7 @@ def main():
                 "global_batch": B * world,
                 "parallelism": f"dp{world} (disjoint problem shards, status all-gather only)",
             },
-            "kernel": ctx.last_kernel_name(),
+            "kernel": kname,
             "kernel_ms": kms,
             "status_counts": status_counts,
             "roofline": {
@@ -469,6 +485,11 @@ def main():
                 "hbm_gbs": hbm_gbs,
                 "traffic_source": os.path.relpath(tj_path, HERE) if traffic else None,
                 "flops_per_problem_iter": F,
+                # the same bound counting only the flops the kernel executes
+                # (Cholesky + triangular solves: no explicit inverse, no A*Li)
+                "flops_executed_per_problem_iter": Fx,
+                "achieved_executed": Fx * iters_per_launch / (kms * 1e-3) / 1e12,
+                "frac_executed": Fx * iters_per_launch / (kms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                 "bytes_per_problem_iter": Bq,
                 "problem_iters_per_launch": iters_per_launch,
             },

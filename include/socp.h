@@ -79,6 +79,16 @@ typedef struct socp_params {
 #define SOCP_F_DEVICE_PTRS 1 /* all data pointers are device (HBM) pointers */
 #define SOCP_F_WARM_START 2  /* x,y,z,s hold the starting iterate: skip the init solve (solver.jl:68-104) */
 #define SOCP_F_FORCE_LARGE 4 /* run the blocked kernel even where the register-resident one applies (testing, tuning) */
+/* Form Li = H^-1 explicitly, as densesolver.jl:48 does (ldiv!(Li, fact, I)),
+ * and use it in every solve (:73,83) -- the reference's operation order.  By
+ * default the kernels factor H = L L' (cholesky!, :47) and replace every
+ * product with Li by two triangular solves (A Li enters as Z = L^-1 A',
+ * S = Z'Z): the same linear algebra in exact arithmetic, far more accurate
+ * near the end of a solve -- where the explicit inverse decides convergence
+ * (a pure LP: chol(H) fails on every problem with it, converges without; see
+ * DESIGN.md §9).  Honoured by socp_batch_solve[_ex], socp_batch_kkt_solve,
+ * socp_dense_create (for all calls of the handle) and socp_ingest_submit. */
+#define SOCP_F_EXPLICIT_INVERSE 8
 
 typedef struct socp_ctx socp_ctx;
 
@@ -171,9 +181,17 @@ int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims,
  *                          for the cholesky(G'G) test at every setup) are
  *                          copied into the handle once;
  *   socp_dense_setup_iter  replaces setup_iter(ss, pr, state, scaling)
- *                          (densesolver.jl:41-52): NT scaling of (s, z), H,
- *                          H^-1, A H^-1 A' and its inverse, kept on the device
- *                          as one factor record per problem;
+ *                          (densesolver.jl:41-52): NT scaling of (s, z), H and
+ *                          its factorisation, kept on the device as one factor
+ *                          record per problem.  By default the record holds
+ *                          the Cholesky factor of H (register kernel, m <= 16:
+ *                          16x16 tiles, L_PP^-1 on the diagonal; blocked
+ *                          kernel: L in place, L_PP^-1 in the diagonal
+ *                          blocks), Z = L^-1 A' and S^-1 for S = Z'Z =
+ *                          A H^-1 A'; H^-1 itself is never formed.  Where m > 16
+ *                          on the register kernel, or with
+ *                          SOCP_F_EXPLICIT_INVERSE, it holds Li = H^-1, A Li
+ *                          (or Li A') and S^-1, as densesolver.jl:48-51 do;
  *                          status[p]: 0, SOCP_CHOL_H_FAILED,
  *                          SOCP_CHOL_S_FAILED or SOCP_DOMAIN_ERROR (where the
  *                          reference throws PosDefException / DomainError);
@@ -368,10 +386,13 @@ int socp_allgather_outcomes(socp_comm* comm, int64_t batch, const int32_t* statu
 int socp_last_kernel_ms(socp_ctx* ctx, float* ms);
 const char* socp_last_kernel_name(socp_ctx* ctx);
 
-/* Testing hook (not part of the reference surface): when set to a device buffer
- * of batch*(2n^2+2k) doubles, socp_batch_kkt_solve dumps per problem the KKT
- * matrix H = G'W^-2G (+A'A) (densesolver.jl:43-46), its inverse Li (:48),
- * lambda and wbar (scalings.jl:1-20).  NULL disables. */
+/* Testing hook (not part of the reference surface; diagnostic build
+ * libsocp_diag.so only): when set to a device buffer of
+ * batch*(2n^2+2k+nm+m^2) doubles, socp_batch_kkt_solve on the register kernel
+ * dumps per problem the KKT matrix H = G'W^-2G (+A'A) (densesolver.jl:43-46),
+ * its inverse Li (:48), lambda and wbar (scalings.jl:1-20), Li A' and S --
+ * on the explicit-inverse path only (m > 16, or SOCP_F_EXPLICIT_INVERSE): the
+ * default Cholesky path never forms Li and dumps nothing.  NULL disables. */
 int socp_debug_set_kkt_dump(double* dev_buf);
 
 /* Diagnostic hook: device buffer of 13 uint64 counters; in the phase-stamp build

@@ -262,7 +262,9 @@ static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
   size_t lds = small_lds_bytes(v->NQ, v->NP, v->MQ);
   if (lds > 160 * 1024) return fail(SOCP_E_UNSUPPORTED, "LDS footprint too large");
   const bool solver = args.mode == MODE_SOLVE;
-  const void* kern = solver ? v->kernel : v->kkt_kernel;
+  // SOCP_F_EXPLICIT_INVERSE: the sweep variants (m <= 16 shapes; larger m sweep anyway)
+  const bool xi = (args.flags & SOCP_F_EXPLICIT_INVERSE) != 0 && v->xi_kernel;
+  const void* kern = xi ? (solver ? v->xi_kernel : v->xi_kkt_kernel) : (solver ? v->kernel : v->kkt_kernel);
   if (lds > 64 * 1024)
     HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = 0;
@@ -277,14 +279,15 @@ static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
   HIPCHK(hipLaunchKernel(kern, dim3((unsigned)blocks), dim3(64), kargs, lds, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
-  ctx->last_name = solver ? v->name : v->kkt_name;
+  ctx->last_name = xi ? (solver ? v->xi_name : v->xi_kkt_name) : (solver ? v->name : v->kkt_name);
   return 0;
 }
 
 static int launch_large(socp_ctx* ctx, const SmallArgs& a, double* rec = nullptr) {
   size_t lds = 0;
   if (!large_fits(a.n, a.m, a.k, a.nc, &lds)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
-  const void* kern = large_kernel_ptr();
+  const bool xi = (a.flags & SOCP_F_EXPLICIT_INVERSE) != 0;
+  const void* kern = large_kernel_ptr(xi);
   HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 512, lds));
@@ -306,7 +309,7 @@ static int launch_large(socp_ctx* ctx, const SmallArgs& a, double* rec = nullptr
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
   HIPCHK(hipLaunchKernel(kern, dim3((unsigned)grid), dim3(512), kargs, lds, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
-  ctx->last_name = large_kernel_name();
+  ctx->last_name = large_kernel_name(xi);
   return 0;
 }
 
@@ -543,6 +546,7 @@ extern "C" int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims, const 
   a.k = k;
   a.nc = dims->ncones;
   a.mode = MODE_KKT;
+  a.flags = flags & SOCP_F_EXPLICIT_INVERSE;
   a.deg = degree;
   a.dbg = g_kkt_debug;
   a.maxit = 1;
@@ -671,7 +675,7 @@ extern "C" int socp_dense_create(socp_ctx* ctx, const socp_dims* dims, const int
   a.deg = degree;
   a.maxit = 1;
   a.sigma_exp = 3;
-  a.flags = flags & SOCP_F_DEVICE_PTRS;
+  a.flags = flags & (SOCP_F_DEVICE_PTRS | SOCP_F_EXPLICIT_INVERSE);
   if (B == 0) {
     *out = h;
     return 0;

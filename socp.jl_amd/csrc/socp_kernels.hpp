@@ -13,6 +13,12 @@ struct SmallVariant {
   const char* name;
   const void* kkt_kernel;  // socp_small_kernel<NQ,NP,MQ,1>: MODE_KKT / MODE_SETUP / MODE_SOLVEKKT
   const char* kkt_name;
+  // SOCP_F_EXPLICIT_INVERSE (KM 2 / 3): the same two with Li = H^-1 formed by
+  // the sweep; NULL where the shape sweeps anyway (m > 16)
+  const void* xi_kernel;
+  const char* xi_name;
+  const void* xi_kkt_kernel;
+  const char* xi_kkt_name;
 };
 
 // table of compiled register-resident variants, ordered by (NQ, NP, MQ)
@@ -91,7 +97,8 @@ struct LargeArgs {
   int64_t wstride;  // doubles per workspace slot
   double* rec;      // MODE_SETUP / MODE_SOLVEKKT: per-problem records (B x r_total), else NULL
 };
-const void* large_kernel_ptr();
-const char* large_kernel_name();
+// xi: the explicit-inverse build (Li = H^-1 by the sweep, SOCP_F_EXPLICIT_INVERSE)
+const void* large_kernel_ptr(bool xi);
+const char* large_kernel_name(bool xi);
 
 }  // namespace socp

@@ -117,7 +117,11 @@ __device__ __forceinline__ d4 tile_mm(const d4& U, const d4& V, d4 C) {
   return C;
 }
 
+// XI (SOCP_F_EXPLICIT_INVERSE): Li = H^-1 by the blocked Gauss-Jordan sweep,
+// the reference's operation order (densesolver.jl:48), instead of H = L L'
+template <bool XI>
 struct Large {
+  static constexpr bool CHOL = SOCP_LG_CHOL && !XI;
   const SmallArgs& a;
   const LargeLayout L;
   const int n, m, k, nc, tid, lane, wv;
@@ -1611,14 +1615,14 @@ struct Large {
     else
       form_H(addAA);
     LSTAMP(SP_SYRK);
-#if SOCP_LG_CHOL
+    if constexpr (CHOL) {
     if (!chol(Hm, L.NPAD)) return ST_CHOL_H;
     if (h_only) return 0;
     LSTAMP(SP_SWEEP_H);
     chol_fwd_multi(Hm, L.NPAD);
     form_S_gram();
     LSTAMP(SP_SCHUR);
-#else
+    } else {
     if (!sweep(Hm, L.NPAD)) return ST_CHOL_H;
     if (h_only) return 0;
     LSTAMP(SP_SWEEP_H);
@@ -1644,7 +1648,7 @@ struct Large {
     }
     BAR();
     LSTAMP(SP_SCHUR);
-#endif
+    }
     if (!sweep(Sm, L.MPAD)) return ST_CHOL_S;
     finalize_sym(Sm, L.MPAD);
     LSTAMP(SP_SCHUR);
@@ -1968,7 +1972,7 @@ struct Large {
       for (int j = tid; j < n; j += NTH) LV(N0 + j) = LV(N0 + j) + At_dot(RP, j);
       BAR();
     }
-#if SOCP_LG_CHOL
+    if constexpr (CHOL) {
     // Li = L^-T L^-1: u = L^-1 n0; m0 = A Li n0 - dy = Z'u - dy; cy = S^-1 m0;
     // cx = Li (n0 + A'm0) = L^-T (u + Z m0)
     trsv_fwd(Hm, L.NPAD, N0, TN);
@@ -1978,7 +1982,7 @@ struct Large {
     BAR();
     z_mv_add(TN, M0, N0);
     trsv_bwd(Hm, L.NPAD, N0, RX);
-#else
+    } else {
     symv(Hm, L.NPAD, N0, TN);
     A_mv(TN, RP, M0);
     symv(Sm, L.MPAD, M0, RY);
@@ -1992,7 +1996,7 @@ struct Large {
       LV(RX + j) = LV(TN + j) + acc;
     }
     BAR();
-#endif
+    }
     gemv_G(RX, -1, K2, K1);
   }
 
@@ -2217,11 +2221,12 @@ struct Large {
   }
 };
 
+template <bool XI>
 __global__ void __launch_bounds__(NTH, 1) socp_large_kernel(LargeArgs args) {
   // the next problem index lives in dynamic LDS (slot 63 of the block-reduction
   // area): no static LDS, so lg_lds starts at LDS address 0 and the staged
   // SYRK's DMA buffers lie in the first 64 KiB
-  Large S(args);
+  Large<XI> S(args);
   S.init_tables();
   const int pslot = S.L.o_red + 63;
   while (true) {
@@ -2237,7 +2242,9 @@ __global__ void __launch_bounds__(NTH, 1) socp_large_kernel(LargeArgs args) {
 
 }  // namespace lg
 
-const void* large_kernel_ptr() { return (const void*)&lg::socp_large_kernel; }
-const char* large_kernel_name() { return "socp_large_kernel"; }
+const void* large_kernel_ptr(bool xi) {
+  return xi ? (const void*)&lg::socp_large_kernel<true> : (const void*)&lg::socp_large_kernel<false>;
+}
+const char* large_kernel_name(bool xi) { return xi ? "socp_large_xi_kernel" : "socp_large_kernel"; }
 
 }  // namespace socp

@@ -214,6 +214,25 @@ __device__ __forceinline__ void a_put(AD& r, double v) {
   asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(r.lo) : "v"((uint32_t)u));
   asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(r.hi) : "v"((uint32_t)(u >> 32)));
 }
+// Load a double from global memory straight into its two AGPRs (gfx950
+// memory instructions take AGPR data operands): no VGPR staging, so every
+// element of G can be in flight at once.  The compiler does not see these
+// loads: a_load_wait() must run before any read of the registers.
+__device__ __forceinline__ void a_load(AD& r, const double* ptr) {
+  asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %2, off offset:4"
+               : "=a"(r.lo), "=a"(r.hi)
+               : "v"(ptr));
+}
+// vmcnt(0), then every loaded AGPR pair passes through an empty volatile asm
+// after it, so no read of G can be scheduled above the wait
+template <int R, int C>
+__device__ __forceinline__ void a_load_wait(AD (&g)[R][C]) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < C; ++j) asm volatile("" : "+a"(g[i][j].lo), "+a"(g[i][j].hi));
+}
 __device__ __forceinline__ double a_get(const AD& r) {
   uint32_t lo, hi;
   asm("v_accvgpr_read_b32 %0, %1" : "=v"(lo) : "a"(r.lo));
@@ -623,7 +642,10 @@ __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok, const H& hoo
 }
 
 
-template <int NQ, int NP, int MQ>
+// XI (SOCP_F_EXPLICIT_INVERSE): Li = H^-1 by the Gauss-Jordan sweep on every
+// shape -- the reference's operation order (densesolver.jl:48 forms Li
+// explicitly) -- instead of the Cholesky path of the m <= 16 shapes.
+template <int NQ, int NP, int MQ, bool XI = false>
 struct Small {
   using SH = Shape<NQ, NP, MQ>;
   static constexpr int NT = NQ * (NQ + 1) / 2;
@@ -651,6 +673,7 @@ struct Small {
   const int lane, g, cl;
   const int n, m, k, nc;
   bool sing;
+  int sing_in = -1;  // the problem's `sing` flag as load_problem read it (-1: none given)
   int64_t dbg_p = 0;
   // compact-layout element info (element i = 64*s + lane): cone, type code
   // (0 POC, 1 SOC head, 2 SOC tail, 3 none), cone offset, scan segment
@@ -676,7 +699,7 @@ struct Small {
   // m <= 16: H = L L' (chol), Z = L^-1 A' in LDS, S = Z'Z; Li is never formed
   // and its products are triangular solves (trsv_fwd / trsv_bwd).  Larger m
   // keep the explicit inverse by the sweep.
-  static constexpr bool CHOL = SOCP_SMALL_CHOL && AL_LDS && !KEEP_AL;
+  static constexpr bool CHOL = SOCP_SMALL_CHOL && AL_LDS && !KEEP_AL && !XI;
 
   __device__ __forceinline__ Small(const SmallArgs& args)
       : a(args), lane(threadIdx.x), g(threadIdx.x >> 4), cl(threadIdx.x & 15),
@@ -732,6 +755,23 @@ struct Small {
     MARK_BEGIN("load_problem");
     LANE_IDS();
     const double* Gp = a.G + p * (int64_t)k * n;
+#ifndef SOCP_GLOAD_AGPR
+#define SOCP_GLOAD_AGPR 1
+#endif
+#if SOCP_GLOAD_AGPR
+    // G -> AGPRs by loads that write the AGPRs themselves: all NP*NQ elements
+    // in flight at once, one HBM round trip (the vector and A loads below ride
+    // along).  Padding (row >= k or col >= n) loads element 0 and is zeroed
+    // after the wait.
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        // padding clamped into the problem's G (no per-element masks kept live)
+        const int row = min(4 * pp + g, k - 1), col = min(16 * q + cl, n - 1);
+        a_load(G[pp][q], Gp + ((int64_t)col * k + row));
+      }
+#else
     // G -> AGPRs.  a_put is an asm statement the scheduler does not move loads
     // across, so the loads are issued in batches of 16 into VGPRs first (one
     // HBM round trip per batch, not per element).  Padding (row >= k or
@@ -760,6 +800,7 @@ struct Small {
         if (e < GT) a_put(G[e / NQ][e % NQ], __longlong_as_double((long long)tmp[t]));
       }
     }
+#endif
     // vectors (n, m <= 64 here, k <= 128), loads first, then the LDS writes
     const double cv = lane < n ? a.c[p * n + lane] : 0.0;
     const double bv = lane < m ? a.b[p * m + lane] : 0.0;
@@ -767,12 +808,24 @@ struct Small {
     const double hv1 = lane + 64 < k ? a.h[p * k + 64 + lane] : 0.0;
     const double* Ap = a.A + p * (int64_t)m * n;
     const int mn = m * n;
-    constexpr int AB = 8;
+    constexpr int AB = 16;  // m*n <= 1024 (C2) in one round
     double av[AB];
 #pragma unroll
     for (int t = 0; t < AB; ++t) av[t] = (64 * t + lane < mn) ? Ap[64 * t + lane] : 0.0;
+    sing_in = a.sing ? (int)a.sing[p] : -1;
     for (int e = lane; e < NKV * SH::KS; e += 64) LDS(O_KV + e) = 0.0;
     for (int e = lane; e < O_U + SH::UAL - O_A; e += 64) LDS(O_A + e) = 0.0;
+#if SOCP_GLOAD_AGPR
+    a_load_wait(G);
+    if (4 * NP > k || 16 * NQ > n) {  // zero the padding (never taken at C1/C2)
+      LANE_IDS();
+#pragma unroll
+      for (int pp = 0; pp < NP; ++pp)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+          if (4 * pp + g >= k || 16 * q + cl >= n) a_put(G[pp][q], 0.0);
+    }
+#endif
     SYNC();
     if (lane < n) LDS(C_ + lane) = cv;
     if (lane < m) LDS(B_ + lane) = bv;
@@ -1781,7 +1834,10 @@ struct Small {
     }
     const bool okH = sweep<NQ, true>(T);
     STAMP(SP_SWEEP_H);
-    if (!okH) return ST_CHOL_H;
+    if (!okH) {
+      clear_tb();
+      return ST_CHOL_H;
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) T[t] = -T[t];
 #ifdef SOCP_DIAG
@@ -1868,6 +1924,7 @@ struct Small {
 #endif
     SYNC();
     const bool okS = sweep<MQ, false>(Sv);
+    clear_tb();  // the sweeps' and A Li's transposes ran in the dead k-vectors (TB_ALIAS)
     STAMP(SP_SCHUR);
     if (!okS) return ST_CHOL_S;
 #pragma unroll
@@ -2408,8 +2465,8 @@ struct Small {
     int phase;
     if (have_sing) {
       phase = after_singtest;
-    } else if (a.sing) {
-      sing = uni((int)a.sing[p]) != 0;
+    } else if (sing_in >= 0) {  // read by load_problem
+      sing = uni(sing_in) != 0;
       phase = after_singtest;
     } else {
       sing = false;
@@ -2631,18 +2688,24 @@ struct Small {
   }
 };
 
+// KM bit 0: the plugin-entry kernel (MODE_KKT / MODE_SETUP / MODE_SOLVEKKT)
+// instead of the solver; bit 1: the explicit-inverse variant (XI above)
 template <int NQ, int NP, int MQ, int KM>
 __global__ void __launch_bounds__(64, 1) socp_small_kernel(SmallArgs args) {
-  Small<NQ, NP, MQ> S(args);
+  Small<NQ, NP, MQ, (KM & 2) != 0> S(args);
   S.init_tables();
   STAMP_START_S(S);
-  while (true) {
-    int p = 0;
-    if (threadIdx.x == 0) p = atomicAdd(args.counter, 1);
-    p = __shfl(p, 0);
-    if ((int64_t)p >= args.B) break;
+  int p = 0;
+  if (threadIdx.x == 0) p = atomicAdd(args.counter, 1);
+  p = __shfl(p, 0);
+  while ((int64_t)p < args.B) {
     S.load_problem(p);
-    S.template run<KM>(p);
+    // the next problem index is fetched while this one solves (after the
+    // loads: returns arrive in order, so it delays no wait of this problem's)
+    int pn = 0;
+    if (threadIdx.x == 0) pn = atomicAdd(args.counter, 1);
+    S.template run<KM & 1>(p);
+    p = __shfl(pn, 0);
   }
   S.flush_stamps();
 }

@@ -22,6 +22,7 @@ const libsocp = get(ENV, "SOCP_AMD_LIB",
 
 const SOCP_F_DEVICE_PTRS = Int32(1)
 const SOCP_F_WARM_START = Int32(2)
+const SOCP_F_EXPLICIT_INVERSE = Int32(8)   # Li = H^-1 formed, the reference's op order (densesolver.jl:48)
 
 struct SocpDims
     batch::Int64
@@ -149,7 +150,8 @@ end
 mutable struct HipDenseSolver <: KKTSolver{HipScaling}
     handle::Ptr{Cvoid}
     status::Vector{Int32}
-    function HipDenseSolver(pr::Problem{C,n,m,k,sing}) where {C,n,m,k,sing}
+    # explicit_inverse=true: SOCP_F_EXPLICIT_INVERSE, Li = H^-1 formed as densesolver.jl:48 does
+    function HipDenseSolver(pr::Problem{C,n,m,k,sing}; explicit_inverse::Bool=false) where {C,n,m,k,sing}
         kind, offs, dim = cone_arrays(pr.cones)
         dims = Ref(SocpDims(1, n, m, k, length(pr.cones)))
         A = Matrix{Float64}(pr.A)   # column-major m x n, as include/socp.h lays it out
@@ -159,7 +161,8 @@ mutable struct HipDenseSolver <: KKTSolver{HipScaling}
         socp_check(ccall((:socp_dense_create, libsocp), Cint,
                          (Ptr{Cvoid}, Ref{SocpDims}, Ptr{Int32}, Ptr{Int32}, Ptr{Int32},
                           Ptr{Float64}, Ptr{Float64}, Ptr{UInt8}, Int32, Ptr{Ptr{Cvoid}}),
-                         socp_ctx(), dims, kind, offs, dim, A, G, singv, Int32(0), h))
+                         socp_ctx(), dims, kind, offs, dim, A, G, singv,
+                         explicit_inverse ? SOCP_F_EXPLICIT_INVERSE : Int32(0), h))
         ss = new(h[], Int32[0])
         finalizer(ss) do x
             x.handle == C_NULL || ccall((:socp_dense_destroy, libsocp), Cint, (Ptr{Cvoid},), x.handle)
@@ -169,8 +172,11 @@ mutable struct HipDenseSolver <: KKTSolver{HipScaling}
     end
 end
 
-# setup_iter(::DenseSolver) (densesolver.jl:41-52): scaling of (s, z), H, H^-1,
-# A H^-1 A' and its factorisation, kept in the handle on the device.
+# setup_iter(::DenseSolver) (densesolver.jl:41-52): scaling of (s, z), H and its
+# factorisation, kept in the handle on the device: by default the Cholesky
+# factor L of H, Z = L^-1 A' and S^-1 (S = Z'Z = A H^-1 A'; H^-1 is never
+# formed), or -- with SOCP_F_EXPLICIT_INVERSE at create, and on m > 16 register
+# shapes -- Li = H^-1, A Li and S^-1 as densesolver.jl:48-51 do.
 function setup_iter(ss::HipDenseSolver, pr::Problem{C,n,m,k,sing}, s::State, scaling::HipScaling) where {C,n,m,k,sing}
     socp_check(ccall((:socp_dense_setup_iter, libsocp), Cint,
                      (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}), ss.handle, s.s, s.z, ss.status))
@@ -243,14 +249,14 @@ end
 
 # ------------------------------------------------------------ batched solve
 """
-    solve_socp_batched(problems; maxit=40, tol=1e-5) -> (states, iters, status)
+    solve_socp_batched(problems; maxit=40, tol=1e-5, explicit_inverse=false) -> (states, iters, status)
 
 `solve_socp` (solver.jl:40-153) for every problem of a vector sharing
 `n, m, k` and the cone tuple, in one device call.  Failures are reported per
 problem in `status` (0 converged, 1 maxit, 2/3 PosDef, 4 domain) instead of
 throwing, so one bad problem does not abort the batch.
 """
-function solve_socp_batched(problems::AbstractVector{<:Problem}; maxit=40, tol=1e-5)
+function solve_socp_batched(problems::AbstractVector{<:Problem}; maxit=40, tol=1e-5, explicit_inverse::Bool=false)
     p0 = problems[1]
     n, m, k = p0.n, p0.m, p0.k
     B = length(problems)
@@ -263,7 +269,7 @@ function solve_socp_batched(problems::AbstractVector{<:Problem}; maxit=40, tol=1
     sing = UInt8[typeof(p).parameters[5] ? 1 : 0 for p in problems]
     x, y, z, s = zeros(B * n), zeros(B * m), zeros(B * k), zeros(B * k)
     iters, status = zeros(Int32, B), zeros(Int32, B)
-    params = Ref(SocpParams(maxit, 3, tol, 0.99, 1e-10, 0, 0))
+    params = Ref(SocpParams(maxit, 3, tol, 0.99, 1e-10, explicit_inverse ? SOCP_F_EXPLICIT_INVERSE : Int32(0), 0))
     dims = Ref(SocpDims(B, n, m, k, length(p0.cones)))
     rc = ccall((:socp_batch_solve, libsocp), Cint,
                (Ptr{Cvoid}, Ref{SocpDims}, Ptr{Int32}, Ptr{Int32}, Ptr{Int32},

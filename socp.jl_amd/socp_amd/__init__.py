@@ -21,7 +21,8 @@ import numpy as np
 
 from . import _lib
 from ._lib import (CHOL_H_FAILED, CHOL_S_FAILED, CONE_POC, CONE_SOC, CONVERGED, DOMAIN_ERROR,
-                   F_DEVICE_PTRS, F_FORCE_LARGE, F_WARM_START, MAXIT, Context, SocpError, default_context,
+                   F_DEVICE_PTRS, F_EXPLICIT_INVERSE, F_FORCE_LARGE, F_WARM_START, MAXIT, Context, SocpError,
+                   default_context,
                    default_params)
 
 __all__ = [
@@ -117,7 +118,8 @@ def _check_sizes(B, **arrays):
 
 
 def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5, step=0.99,
-                sigma_exp=3, init_eps=1e-10, warm=None, ctx=None, res=False, out=None, force_large=False):
+                sigma_exp=3, init_eps=1e-10, warm=None, ctx=None, res=False, out=None, force_large=False,
+                explicit_inverse=False):
     """Solve a batch of independent problems (same dims and cone structure).
 
     Arrays follow include/socp.h: per-problem column-major A (m x n), G (k x n)
@@ -125,7 +127,10 @@ def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5,
     host staging buffers; torch CUDA tensors are used in place (device mode,
     stream-ordered on the context's stream; call ctx.sync() before reading).
     force_large runs the blocked kernel (socp_large.hip) even where the
-    register-resident one applies.  Returns dict(x, y, z, s, iters, status[, res]).
+    register-resident one applies.  explicit_inverse (SOCP_F_EXPLICIT_INVERSE)
+    forms Li = H^-1 as densesolver.jl:48 does -- the reference's op order --
+    instead of the Cholesky factor + triangular solves of the m <= 16 shapes.
+    Returns dict(x, y, z, s, iters, status[, res]).
     """
     L = _lib.load()
     kind, offs, dim = cone_arrays(cones)
@@ -146,6 +151,8 @@ def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5,
         flags |= F_WARM_START
     if force_large:
         flags |= F_FORCE_LARGE
+    if explicit_inverse:
+        flags |= F_EXPLICIT_INVERSE
     P = default_params(maxit=maxit, tol=tol, step=step, sigma_exp=sigma_exp, init_eps=init_eps,
                        flags=flags)
     if dev:
@@ -190,7 +197,8 @@ def batch_solve(cones, n, m, k, c, A, b, G, h, sing=None, *, maxit=40, tol=1e-5,
     return out
 
 
-def batch_kkt_solve(cones, n, m, k, A, G, sing, s, z, dx, dy, dz, ds, *, ctx=None, force_large=False):
+def batch_kkt_solve(cones, n, m, k, A, G, sing, s, z, dx, dy, dz, ds, *, ctx=None, force_large=False,
+                    explicit_inverse=False):
     """One KKT solve per problem at iterate (s, z): scaling + setup_iter + solve_kkt
     (densesolver.jl:41-90) on the GPU.  Host (numpy) arrays.  Returns dict(cx,cy,cz,cs,status)."""
     L = _lib.load()
@@ -210,7 +218,8 @@ def batch_kkt_solve(cones, n, m, k, A, G, sing, s, z, dx, dy, dz, ds, *, ctx=Non
                                 p(_host(A) if m else None), p(_host(G)), p(sg), p(_host(s)), p(_host(z)),
                                 p(_host(dx)), p(_host(dy) if m else None), p(_host(dz)), p(_host(ds)),
                                 p(cx), p(cy if m else None), p(cz), p(cs), p(st),
-                                F_FORCE_LARGE if force_large else 0)
+                                (F_FORCE_LARGE if force_large else 0)
+                                | (F_EXPLICIT_INVERSE if explicit_inverse else 0))
     _lib.check(rc)
     return dict(cx=cx, cy=cy[:B * m], cz=cz, cs=cs, status=st)
 
@@ -233,7 +242,7 @@ class DenseHandle:
     def _fn(self, name):
         return getattr(_lib.load(), f"{self._pfx}_{name}")
 
-    def __init__(self, cones, n, m, k, A, G, sing=None, *, ctx=None, force_large=False):
+    def __init__(self, cones, n, m, k, A, G, sing=None, *, ctx=None, force_large=False, explicit_inverse=False):
         self.cones, self.n, self.m, self.k = cones, n, m, k
         self.kind, self.offs, self.dim = cone_arrays(cones)
         B = _size(G) // (k * n)
@@ -243,7 +252,8 @@ class DenseHandle:
         self.B = B
         self.ctx = ctx or default_context()
         self.dev = _is_torch(G)
-        flags = (F_DEVICE_PTRS if self.dev else 0) | (F_FORCE_LARGE if force_large else 0)
+        flags = ((F_DEVICE_PTRS if self.dev else 0) | (F_FORCE_LARGE if force_large else 0)
+                 | (F_EXPLICIT_INVERSE if explicit_inverse else 0))
         if self.dev:
             self.ctx.bind_torch_stream()
             arrs = (A if m else None, G, sing)

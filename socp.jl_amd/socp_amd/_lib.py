@@ -18,7 +18,7 @@ HEADER = os.path.join(os.path.dirname(_PKG_ROOT), "include", "socp.h")
 SOCP_OK, SOCP_E_INVALID, SOCP_E_UNSUPPORTED, SOCP_E_HIP, SOCP_E_NOMEM = 0, -1, -2, -3, -4
 CONVERGED, MAXIT, CHOL_H_FAILED, CHOL_S_FAILED, DOMAIN_ERROR = 0, 1, 2, 3, 4
 CONE_POC, CONE_SOC = 0, 1
-F_DEVICE_PTRS, F_WARM_START, F_FORCE_LARGE = 1, 2, 4
+F_DEVICE_PTRS, F_WARM_START, F_FORCE_LARGE, F_EXPLICIT_INVERSE = 1, 2, 4, 8
 
 EXPORTED = [
     "socp_last_error", "socp_version", "socp_params_default", "socp_ctx_create",
