@@ -214,25 +214,6 @@ __device__ __forceinline__ void a_put(AD& r, double v) {
   asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(r.lo) : "v"((uint32_t)u));
   asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(r.hi) : "v"((uint32_t)(u >> 32)));
 }
-// Load a double from global memory straight into its two AGPRs (gfx950
-// memory instructions take AGPR data operands): no VGPR staging, so every
-// element of G can be in flight at once.  The compiler does not see these
-// loads: a_load_wait() must run before any read of the registers.
-__device__ __forceinline__ void a_load(AD& r, const double* ptr) {
-  asm volatile("global_load_dword %0, %2, off\n\tglobal_load_dword %1, %2, off offset:4"
-               : "=a"(r.lo), "=a"(r.hi)
-               : "v"(ptr));
-}
-// vmcnt(0), then every loaded AGPR pair passes through an empty volatile asm
-// after it, so no read of G can be scheduled above the wait
-template <int R, int C>
-__device__ __forceinline__ void a_load_wait(AD (&g)[R][C]) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < R; ++i)
-#pragma unroll
-    for (int j = 0; j < C; ++j) asm volatile("" : "+a"(g[i][j].lo), "+a"(g[i][j].hi));
-}
 __device__ __forceinline__ double a_get(const AD& r) {
   uint32_t lo, hi;
   asm("v_accvgpr_read_b32 %0, %1" : "=v"(lo) : "a"(r.lo));
@@ -673,7 +654,6 @@ struct Small {
   const int lane, g, cl;
   const int n, m, k, nc;
   bool sing;
-  int sing_in = -1;  // the problem's `sing` flag as load_problem read it (-1: none given)
   int64_t dbg_p = 0;
   // compact-layout element info (element i = 64*s + lane): cone, type code
   // (0 POC, 1 SOC head, 2 SOC tail, 3 none), cone offset, scan segment
@@ -751,27 +731,17 @@ struct Small {
     }
   }
 
+#ifndef SOCP_KO
+#define SOCP_KO 0  // timing knock-outs (tuning builds only; results are wrong): 1 G loaded once per wave,
+                   // 2 no residuals, 4 no compute_U, 8 no S factorisation
+#endif
+  bool ko_gloaded = false;
   __device__ __forceinline__ void load_problem(int64_t p) {
     MARK_BEGIN("load_problem");
     LANE_IDS();
     const double* Gp = a.G + p * (int64_t)k * n;
-#ifndef SOCP_GLOAD_AGPR
-#define SOCP_GLOAD_AGPR 1
-#endif
-#if SOCP_GLOAD_AGPR
-    // G -> AGPRs by loads that write the AGPRs themselves: all NP*NQ elements
-    // in flight at once, one HBM round trip (the vector and A loads below ride
-    // along).  Padding (row >= k or col >= n) loads element 0 and is zeroed
-    // after the wait.
-#pragma unroll
-    for (int pp = 0; pp < NP; ++pp)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        // padding clamped into the problem's G (no per-element masks kept live)
-        const int row = min(4 * pp + g, k - 1), col = min(16 * q + cl, n - 1);
-        a_load(G[pp][q], Gp + ((int64_t)col * k + row));
-      }
-#else
+    if (!(SOCP_KO & 1) || !ko_gloaded) {
+    ko_gloaded = true;
     // G -> AGPRs.  a_put is an asm statement the scheduler does not move loads
     // across, so the loads are issued in batches of 16 into VGPRs first (one
     // HBM round trip per batch, not per element).  Padding (row >= k or
@@ -800,7 +770,7 @@ struct Small {
         if (e < GT) a_put(G[e / NQ][e % NQ], __longlong_as_double((long long)tmp[t]));
       }
     }
-#endif
+    }
     // vectors (n, m <= 64 here, k <= 128), loads first, then the LDS writes
     const double cv = lane < n ? a.c[p * n + lane] : 0.0;
     const double bv = lane < m ? a.b[p * m + lane] : 0.0;
@@ -808,24 +778,12 @@ struct Small {
     const double hv1 = lane + 64 < k ? a.h[p * k + 64 + lane] : 0.0;
     const double* Ap = a.A + p * (int64_t)m * n;
     const int mn = m * n;
-    constexpr int AB = 16;  // m*n <= 1024 (C2) in one round
+    constexpr int AB = 8;
     double av[AB];
 #pragma unroll
     for (int t = 0; t < AB; ++t) av[t] = (64 * t + lane < mn) ? Ap[64 * t + lane] : 0.0;
-    sing_in = a.sing ? (int)a.sing[p] : -1;
     for (int e = lane; e < NKV * SH::KS; e += 64) LDS(O_KV + e) = 0.0;
     for (int e = lane; e < O_U + SH::UAL - O_A; e += 64) LDS(O_A + e) = 0.0;
-#if SOCP_GLOAD_AGPR
-    a_load_wait(G);
-    if (4 * NP > k || 16 * NQ > n) {  // zero the padding (never taken at C1/C2)
-      LANE_IDS();
-#pragma unroll
-      for (int pp = 0; pp < NP; ++pp)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q)
-          if (4 * pp + g >= k || 16 * q + cl >= n) a_put(G[pp][q], 0.0);
-    }
-#endif
     SYNC();
     if (lane < n) LDS(C_ + lane) = cv;
     if (lane < m) LDS(B_ + lane) = bv;
@@ -1377,30 +1335,44 @@ struct Small {
   }
 
   // U[c,:] = (sum_{i in cone c} w_i G[i,:]) / (1+wb0), w_head = -(1+wb0), w_tail = wb_i
+  // The cone descriptors come from the kernel arguments (scalar loads); the
+  // row steps a cone covers are taken four at a time, their four weight reads
+  // issued together (one LDS round trip per four row steps), the weights
+  // masked branch-free.
   __device__ __forceinline__ void compute_U() {
     MARK_BEGIN("compute_U");
     LANE_IDS();
     for (int c = 0; c < nc; ++c) {
-      if (uni((int)LDS(O_CKIND + c)) != SOC_K) continue;
-      const int o = uni((int)LDS(O_COFF + c)), d = uni((int)LDS(O_CDIM + c));
-      const double wb0 = LDS(WB + o);
+      if (a.cones.kind[c] != SOC_K) continue;
+      const int o = a.cones.offs[c], d = a.cones.dim[c];
+      const double hw = -(1.0 + LDS(WB + o));  // the head row's weight
+      const int p0 = o >> 2, p1 = (o + d + 3) >> 2;  // row steps [p0, p1) meet the cone
       double acc[NQ];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
 #pragma unroll
-      for (int pp = 0; pp < NP; ++pp) {
-        if (4 * pp + 3 >= o && 4 * pp < o + d) {
-          const int row = 4 * pp + g;
-          const bool in = row >= o && row < o + d;
-          const double w = in ? (row == o ? -(1.0 + wb0) : LDS(WB + row)) : 0.0;
+      for (int pb = 0; pb < NP; pb += 4) {
+        if (pb + 4 <= p0 || pb >= p1) continue;  // wave-uniform
+        constexpr int U4 = 4;
+        double w[U4];
 #pragma unroll
-          for (int q = 0; q < NQ; ++q) acc[q] = fma(w, a_get(G[pp][q]), acc[q]);
+        for (int u = 0; u < U4; ++u) {
+          const int row = 4 * (pb + u) + g;  // < KP: in the LDS k-vector
+          w[u] = (pb + u < NP) ? LDS(WB + row) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U4; ++u) {
+          const int row = 4 * (pb + u) + g;
+          const bool in = row >= o && row < o + d;
+          const double wu = in ? (row == o ? hw : w[u]) : 0.0;
+          if (pb + u < NP) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) acc[q] = fma(wu, a_get(G[pb + u < NP ? pb + u : 0][q]), acc[q]);
+          }
         }
       }
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        acc[q] = rows_sum(acc[q]);
-      }
+      for (int q = 0; q < NQ; ++q) acc[q] = rows_sum(acc[q]);
       if (g == 0) {
         const double inv = LDS(cc(CC_I1, c));
 #pragma unroll
@@ -1805,7 +1777,7 @@ struct Small {
     MARK_BEGIN("factor");
     LANE_IDS();
     STAMP(SP_OTHER);
-    if (!identity) compute_U();
+    if (!identity && !(SOCP_KO & 4)) compute_U();
     STAMP(SP_U);
     form_H(addAA);
     SYNC();
@@ -1825,7 +1797,7 @@ struct Small {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (g + 4 * r == cl && cl >= m) Sv[0][r] = 1.0;
-      const bool okS = sweep<1, false>(Sv);
+      const bool okS = (SOCP_KO & 8) ? true : sweep<1, false>(Sv);
       clear_tb();
       STAMP(SP_SCHUR);
       if (!okS) return ST_CHOL_S;
@@ -2224,9 +2196,17 @@ struct Small {
       for (int q = 0; q < NQ; ++q) acc[q] = rows_sum(acc[q]);
     }
 #else
-    gemv_Gt(Z_, acc);
+    if (SOCP_KO & 32) {
+      for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+    } else {
+      gemv_Gt(Z_, acc);
+    }
 #endif
-    At_mv(Y_, at);
+    if (SOCP_KO & 128) {
+      for (int q = 0; q < NQ; ++q) at[q] = 0.0;
+    } else {
+      At_mv(Y_, at);
+    }
     double d2 = 0.0, zs = 0.0;
     if (g == 0) {
 #pragma unroll
@@ -2239,16 +2219,22 @@ struct Small {
         }
       }
     }
-    const double p2 = A_mv(X_, B_, RP);
+    const double p2 = (SOCP_KO & 128) ? 0.0 : A_mv(X_, B_, RP);
 #if SOCP_RESID_MERGE
     SYNC();
 #else
-    gemv_G(X_, S_, H_, DZ);
+    if (!(SOCP_KO & 16)) gemv_G(X_, S_, H_, DZ);
 #endif
     for (int i = lane; i < k; i += 64) zs += LDS(Z_ + i) * LDS(S_ + i);
-    nd = sqrt(wsum(d2));
-    np_ = sqrt(wsum(p2));
-    gap = wsum(zs);
+    if (SOCP_KO & 64) {
+      nd = np_ = gap = d2 + p2 + zs;
+    } else {
+      double r3[3] = {d2, p2, zs};  // the three whole-wave sums in one interleaved scan
+      dpp_scan<3>(r3, lane, 0, false);
+      nd = sqrt(readlane_d(r3[0], 63));
+      np_ = sqrt(readlane_d(r3[1], 63));
+      gap = readlane_d(r3[2], 63);
+    }
   }
 
   // The matrix part of solve_kkt(::DenseSolver) (densesolver.jl:66-85), between
@@ -2260,7 +2246,11 @@ struct Small {
     LANE_IDS();
     {
       double acc[NQ], at[NQ];
-      gemv_Gt(T2, acc);
+      if (SOCP_KO & 512) {
+        for (int q = 0; q < NQ; ++q) acc[q] = LDS(T2 + 16 * q + cl);
+      } else {
+        gemv_Gt(T2, acc);
+      }
       if (sing) At_mv(RP, at);
       if (g == 0) {
 #pragma unroll
@@ -2274,19 +2264,31 @@ struct Small {
     }
     SYNC();
     STAMP_X(4);
-    if constexpr (CHOL)
-      trsv_fwd(N0, TN);    // t = L^-1 n0
-    else
+    if constexpr (CHOL) {
+      if (SOCP_KO & 256) {
+        for (int j = lane; j < NPAD; j += 64) LDS(TN + j) = LDS(N0 + j);
+        SYNC();
+      } else {
+        trsv_fwd(N0, TN);    // t = L^-1 n0
+      }
+    } else
       symv<NQ>(T, N0, TN);   // Li n0
     STAMP_X(5);
-    if constexpr (CHOL)
+    if (SOCP_KO & 2048) {
+      for (int j = lane; j < m; j += 64) LDS(M0 + j) = LDS(TN + j);
+    } else if constexpr (CHOL)
       A_mv(TN, RP, M0, O_AL);  // m0 = A Li n0 - dy = Z't - dy
     else if constexpr (AL_LDS)
       A_mv(N0, RP, M0, O_AL);  // m0 = (A Li) n0 - dy: no wait for Li n0
     else
       A_mv(TN, RP, M0);        // m0 = A (Li n0) - dy
     SYNC();
-    symv<MQ>(Sv, M0, RY);  // cy = S^-1 m0
+    if (SOCP_KO & 2048) {
+      for (int j = lane; j < m; j += 64) LDS(RY + j) = LDS(M0 + j);
+      SYNC();
+    } else {
+      symv<MQ>(Sv, M0, RY);  // cy = S^-1 m0
+    }
     if (lane < m) LDS(M0 + lane) = (sing && !init) ? LDS(RP + lane) - LDS(RY + lane) : -LDS(RY + lane);
     SYNC();
     STAMP_X(6);
@@ -2297,13 +2299,19 @@ struct Small {
       // cx = Li (n0 + A'm0) = Li n0 + (A Li)' m0: one Li product per solve
       // (CHOL: cx = L^-T (t + Z m0))
       double at[NQ];
-      At_mv(M0, at, O_AL);
+      if (SOCP_KO & 2048) {
+        for (int q = 0; q < NQ; ++q) at[q] = 0.0;
+      } else {
+        At_mv(M0, at, O_AL);
+      }
       if (g == 0) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) LDS(RX + 16 * q + cl) = LDS(TN + 16 * q + cl) + at[q];
       }
       SYNC();
-      if constexpr (CHOL) trsv_bwd(RX, RX);
+      if constexpr (CHOL) {
+        if (!(SOCP_KO & 256)) trsv_bwd(RX, RX);
+      }
       STAMP_X(7);
     } else {
       double at[NQ];
@@ -2315,7 +2323,12 @@ struct Small {
       SYNC();
       symv<NQ>(T, N0, RX);  // cx = Li n0
     }
-    gemv_G(RX, -1, K2, K1);
+    if (SOCP_KO & 1024) {
+      for (int i = lane; i < k; i += 64) LDS(K1 + i) = LDS(RX + (i & 63)) - LDS(K2 + i);
+      SYNC();
+    } else {
+      gemv_G(RX, -1, K2, K1);
+    }
   }
 
   // out[j] = add[j] + ((A Li)' v)[j]: per tile column, an in-lane sum over the
@@ -2465,8 +2478,8 @@ struct Small {
     int phase;
     if (have_sing) {
       phase = after_singtest;
-    } else if (sing_in >= 0) {  // read by load_problem
-      sing = uni(sing_in) != 0;
+    } else if (a.sing) {
+      sing = uni((int)a.sing[p]) != 0;
       phase = after_singtest;
     } else {
       sing = false;
@@ -2525,7 +2538,11 @@ struct Small {
         case MP_ITER: {  // residuals (solver.jl:109-118), compute_scaling (:106), exit test (:122)
           MARK_BEGIN("case MP_ITER");
           STAMP(SP_OTHER);
-          residuals(nd, np_, gap);
+          if (SOCP_KO & 2) {
+            nd = np_ = gap = 1.0;
+          } else {
+            residuals(nd, np_, gap);
+          }
           STAMP(SP_RESID);
           if (it >= a.maxit) {
             done = true;
@@ -2695,17 +2712,13 @@ __global__ void __launch_bounds__(64, 1) socp_small_kernel(SmallArgs args) {
   Small<NQ, NP, MQ, (KM & 2) != 0> S(args);
   S.init_tables();
   STAMP_START_S(S);
-  int p = 0;
-  if (threadIdx.x == 0) p = atomicAdd(args.counter, 1);
-  p = __shfl(p, 0);
-  while ((int64_t)p < args.B) {
+  while (true) {
+    int p = 0;
+    if (threadIdx.x == 0) p = atomicAdd(args.counter, 1);
+    p = __shfl(p, 0);
+    if ((int64_t)p >= args.B) break;
     S.load_problem(p);
-    // the next problem index is fetched while this one solves (after the
-    // loads: returns arrive in order, so it delays no wait of this problem's)
-    int pn = 0;
-    if (threadIdx.x == 0) pn = atomicAdd(args.counter, 1);
     S.template run<KM & 1>(p);
-    p = __shfl(pn, 0);
   }
   S.flush_stamps();
 }

@@ -138,6 +138,8 @@ def timed_shard_steps(solve_shard, steps: int, warmup: int, sync=None):
     import time
     import torch
     import torch.distributed as dist
+    if steps < 1:
+        raise ValueError(f"steps must be >= 1 (got {steps})")
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
     sync = sync or (lambda: None)
     st = {"out": None, "gathered": None}
@@ -154,16 +156,19 @@ def timed_shard_steps(solve_shard, steps: int, warmup: int, sync=None):
     if world > 1:
         dist.barrier()
     step_ms = []
+    it_sum = None  # executed iterations summed step by step (on the device for device results: no sync)
     t0 = time.perf_counter()
     for _ in range(steps):
         t1 = time.perf_counter()
         step()
+        s_ = st["out"]["iters"].sum()
+        it_sum = s_ if it_sum is None else it_sum + s_
         step_ms.append((time.perf_counter() - t1) * 1e3)
     sync()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    iters_local = int(st["out"]["iters"].sum().item()) * steps
+    iters_local = int(it_sum.item()) if hasattr(it_sum, "item") else int(it_sum)
     iters_total = iters_local
     if world > 1:
         dev = st["out"]["iters"].device
