@@ -114,12 +114,13 @@ int socp_ctx_reset_stream(socp_ctx* ctx);
 /* 1 if a compiled kernel accepts the dims: the register-resident kernel (one
  * wavefront per problem, <= 8 cones, m <= 64; k <= 128 for n <= 48, k <= 96
  * for 48 < n <= 64: the compiled variant table, socp.jl_amd/csrc/gen_inst.py)
- * or the blocked kernel (n, m <= 512, <= 64 cones, the problem's vectors within
- * the 160 KiB LDS of a CU -- C4, n=512 m=64 k=640, uses 126 KiB; one
- * 512-thread workgroup per problem), which also takes every register-kernel
- * shape it can hold.  Other shapes return SOCP_E_UNSUPPORTED from the solve
- * entries.  Every entry rejects batch > 2^31-1 (device problem indices are
- * int32). */
+ * or the blocked kernel (n, m <= 512, <= 64 cones, any k; one 512-thread
+ * workgroup per problem), which also takes every register-kernel shape.  The
+ * blocked kernel keeps the problem's vectors in the 160 KiB LDS of a CU when
+ * they fit (C4, n=512 m=64 k=640, uses 126 KiB) and in its HBM workspace slot
+ * otherwise (e.g. k = 1000 at n = 512).  Other shapes return
+ * SOCP_E_UNSUPPORTED from the solve entries.  Every entry rejects batch >
+ * 2^31-1 (device problem indices are int32). */
 int socp_supported(const socp_dims* dims);
 
 /* Batched solve: replaces solve_socp(prob, SolverState(prob, DenseSolver(prob)))

@@ -224,13 +224,17 @@ static const SmallVariant* pick_variant(int n, int m, int k) {
 }
 
 // The blocked kernel (socp_large.hip): n, m <= 512 (a swept panel row is held
-// in registers) and the problem's vectors within the 160 KiB LDS of a CU.
-static bool large_fits(int n, int m, int k, int nc, size_t* lds_bytes) {
+// in registers).  The problem's vectors live in the 160 KiB LDS of a CU when
+// they fit; otherwise (e.g. k = 1000 at n = 512) in the workgroup's slot of the
+// HBM workspace (*gv: the GV kernels), with only the problem index in LDS.
+static bool large_fits(int n, int m, int k, int nc, size_t* lds_bytes, bool* gv = nullptr) {
   const LargeLayout L = large_layout(n, m, k);
   if (L.NPAD > 64 * LARGE_NB_MAX || L.MPAD > 64 * LARGE_NB_MAX || nc > MAXC) return false;
-  const size_t lds = (size_t)L.total * sizeof(double);
-  if (lds + 64 > 160 * 1024) return false;
+  size_t lds = (size_t)L.total * sizeof(double);
+  const bool g = lds + 64 > 160 * 1024;
+  if (g) lds = 64 * sizeof(double);
   if (lds_bytes) *lds_bytes = lds;
+  if (gv) *gv = g;
   return true;
 }
 
@@ -242,7 +246,7 @@ extern "C" int socp_supported(const socp_dims* d) {
 
 static const char* kUnsupported =
     "dims outside both kernels (register-resident: n, m <= 64, k <= 128, <= 8 cones; "
-    "blocked: n, m <= 512, <= 64 cones, k-vectors within the 160 KiB LDS)";
+    "blocked: n, m <= 512, <= 64 cones)";
 
 // ---------------------------------------------------------------- launch
 static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_DIAG builds)
@@ -285,9 +289,10 @@ static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
 
 static int launch_large(socp_ctx* ctx, const SmallArgs& a, double* rec = nullptr) {
   size_t lds = 0;
-  if (!large_fits(a.n, a.m, a.k, a.nc, &lds)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
+  bool gv = false;
+  if (!large_fits(a.n, a.m, a.k, a.nc, &lds, &gv)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
   const bool xi = (a.flags & SOCP_F_EXPLICIT_INVERSE) != 0;
-  const void* kern = large_kernel_ptr(xi);
+  const void* kern = large_kernel_ptr(xi, gv);
   HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 512, lds));
@@ -309,7 +314,7 @@ static int launch_large(socp_ctx* ctx, const SmallArgs& a, double* rec = nullptr
   HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
   HIPCHK(hipLaunchKernel(kern, dim3((unsigned)grid), dim3(512), kargs, lds, ctx->stream));
   HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
-  ctx->last_name = large_kernel_name(xi);
+  ctx->last_name = large_kernel_name(xi, gv);
   return 0;
 }
 

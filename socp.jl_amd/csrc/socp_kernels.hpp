@@ -35,7 +35,7 @@ struct LargeLayout {
   int o_rc, o_cc, o_kvd, o_kvl, o_nv, o_mv, o_row, o_rv, o_part, o_red, o_fx, total;
   int sy;  // 1: the staged SYRK's four chunk buffers fit (socp_large.hip form_H_staged_g)
   // workspace-slot offsets (doubles)
-  int64_t w_x, w_h, w_ap, w_at, w_yp, w_rv, w_t, w_s, w_v, w_total;
+  int64_t w_x, w_h, w_ap, w_at, w_yp, w_rv, w_t, w_s, w_v, w_lv, w_total;
   // per-problem factor record (socp_dense handles): what solve_kkt reads
   int64_t r_h, r_ap, r_at, r_t, r_s, r_v, r_total;
 };
@@ -80,6 +80,7 @@ __host__ __device__ inline LargeLayout large_layout(int n, int m, int k) {
   L.w_t = w;  w += large_al((int64_t)L.NPAD * L.MPAD);  // Li A'
   L.w_s = w;  w += large_al((int64_t)L.MPAD * L.MPAD);  // S -> S^-1
   L.w_v = w;  w += large_al(3 * (int64_t)L.KP + 12 * MAXC + 8);  // LAM WB CA, CC_*, sing, status
+  L.w_lv = w; w += large_al(L.total);  // the vectors themselves when they exceed the LDS (GV kernels)
   L.w_total = w;
   w = 0;
   L.r_h = w;  w += large_al((int64_t)L.NPAD * L.NPAD);
@@ -97,8 +98,10 @@ struct LargeArgs {
   int64_t wstride;  // doubles per workspace slot
   double* rec;      // MODE_SETUP / MODE_SOLVEKKT: per-problem records (B x r_total), else NULL
 };
-// xi: the explicit-inverse build (Li = H^-1 by the sweep, SOCP_F_EXPLICIT_INVERSE)
-const void* large_kernel_ptr(bool xi);
-const char* large_kernel_name(bool xi);
+// xi: the explicit-inverse build (Li = H^-1 by the sweep, SOCP_F_EXPLICIT_INVERSE);
+// gv: the problem's vectors in the HBM workspace instead of LDS (shapes whose
+// vectors exceed a CU's 160 KiB of LDS)
+const void* large_kernel_ptr(bool xi, bool gv);
+const char* large_kernel_name(bool xi, bool gv);
 
 }  // namespace socp

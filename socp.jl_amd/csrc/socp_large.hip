@@ -48,7 +48,10 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const dbl2 gcdbl2;
 
 extern __shared__ double lg_lds[];
-#define LV(i) lg_lds[(i)]
+// The problem's vectors: in LDS, or (GV: shapes whose vectors exceed the
+// 160 KiB of a CU's LDS, e.g. k = 1000 at n = 512) in the workgroup's slot of
+// the HBM workspace -- Large::lvref picks at compile time.
+#define LV(i) lvref(i)
 // Workgroup barrier.  Global stores read by other wavefronts after it (the
 // workspace) are drained first; all waves of the workgroup share the CU's L1.
 #define BAR()                                       \
@@ -58,9 +61,13 @@ extern __shared__ double lg_lds[];
   } while (0)
 // LDS-only barrier: the global stores in flight stay in flight (a
 // __syncthreads would drain them first, one store round trip per barrier)
-#define LDS_BAR()                                                 \
-  do {                                                            \
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); \
+#define LDS_BAR()                                                     \
+  do {                                                                \
+    if constexpr (GV) {                                               \
+      BAR(); /* the vectors are global memory: drain the stores too */ \
+    } else {                                                          \
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");    \
+    }                                                                 \
   } while (0)
 
 // Diagnostic build (-DSOCP_DIAG): thread 0 adds per-phase s_memtime deltas
@@ -69,7 +76,7 @@ extern __shared__ double lg_lds[];
 #ifdef SOCP_DIAG
 #define LSTAMP(i)                                                                          \
   do {                                                                                     \
-    if (tid == 0) {                                                                        \
+    if (!GV && tid == 0) {                                                                 \
       const uint64_t t_ = __builtin_amdgcn_s_memtime();                                    \
       reinterpret_cast<unsigned long long*>(lg_lds + L.o_red + 16)[(i)] += t_ - st_last;    \
       st_last = t_;                                                                        \
@@ -118,10 +125,18 @@ __device__ __forceinline__ d4 tile_mm(const d4& U, const d4& V, d4 C) {
 }
 
 // XI (SOCP_F_EXPLICIT_INVERSE): Li = H^-1 by the blocked Gauss-Jordan sweep,
-// the reference's operation order (densesolver.jl:48), instead of H = L L'
-template <bool XI>
+// the reference's operation order (densesolver.jl:48), instead of H = L L'.
+// GV: the vectors in global memory (LV above).
+template <bool XI, bool GV>
 struct Large {
   static constexpr bool CHOL = SOCP_LG_CHOL && !XI;
+  gdbl* gvec = nullptr;  // GV: this workgroup's vector region (workspace slot)
+  __device__ __forceinline__ auto& lvref(int i) const {
+    if constexpr (GV)
+      return gvec[i];
+    else
+      return lg_lds[i];
+  }
   const SmallArgs& a;
   const LargeLayout L;
   const int n, m, k, nc, tid, lane, wv;
@@ -195,6 +210,7 @@ struct Large {
     Tm = ws + L.w_t;
     Sm = ws + L.w_s;
     Vr = ws + L.w_v;
+    if constexpr (GV) gvec = ws + L.w_lv;
   }
   // the matrices solve_kkt reads move to problem p's record
   __device__ void set_record(int64_t p) {
@@ -285,7 +301,7 @@ struct Large {
   __device__ void flush_stamps() {
 #ifdef SOCP_DIAG
     BAR();
-    if (tid == 0 && a.stamps) {
+    if (!GV && tid == 0 && a.stamps) {
       const unsigned long long* st = reinterpret_cast<const unsigned long long*>(lg_lds + L.o_red + 16);
       for (int i = 0; i <= NSTAMP + NSUBSTAMP; ++i) atomicAdd(a.stamps + i, st[i]);
     }
@@ -1048,6 +1064,7 @@ struct Large {
   }
   // the LDS-DMA destination (M0) kept inside the first 64 KiB
   __device__ bool staged_ok() const {
+    if constexpr (GV) return false;  // the staged SYRK's buffers are LDS
     const unsigned lbase = (unsigned)(uintptr_t)((__attribute__((address_space(3))) double*)(lg_lds + L.o_kvd));
     return SOCP_LG_STAGED && L.sy && lbase + 128u * (unsigned)L.NPAD <= 65536u;
   }
@@ -2221,18 +2238,19 @@ struct Large {
   }
 };
 
-template <bool XI>
+template <bool XI, bool GV>
 __global__ void __launch_bounds__(NTH, 1) socp_large_kernel(LargeArgs args) {
   // the next problem index lives in dynamic LDS (slot 63 of the block-reduction
-  // area): no static LDS, so lg_lds starts at LDS address 0 and the staged
-  // SYRK's DMA buffers lie in the first 64 KiB
-  Large<XI> S(args);
+  // area; GV: slot 0 of the kernel's small LDS): no static LDS, so lg_lds
+  // starts at LDS address 0 and the staged SYRK's DMA buffers lie in the
+  // first 64 KiB
+  Large<XI, GV> S(args);
   S.init_tables();
-  const int pslot = S.L.o_red + 63;
+  const int pslot = GV ? 0 : S.L.o_red + 63;
   while (true) {
-    if (threadIdx.x == 0) LV(pslot) = (double)atomicAdd(args.a.counter, 1);
+    if (threadIdx.x == 0) lg_lds[pslot] = (double)atomicAdd(args.a.counter, 1);
     __syncthreads();
-    const int64_t p = (int64_t)LV(pslot);
+    const int64_t p = (int64_t)lg_lds[pslot];
     __syncthreads();  // everyone has read pidx before thread 0 overwrites it
     if (p >= args.a.B) break;
     S.run(p);
@@ -2240,11 +2258,24 @@ __global__ void __launch_bounds__(NTH, 1) socp_large_kernel(LargeArgs args) {
   S.flush_stamps();
 }
 
+#if SOCP_LG_GV_TU
+// the global-vector kernels (socp_large_gv.o: this file with SOCP_LG_GV_TU=1)
+template __global__ void socp_large_kernel<false, true>(LargeArgs);
+template __global__ void socp_large_kernel<true, true>(LargeArgs);
+}  // namespace lg
+#else
+extern template __global__ void socp_large_kernel<false, true>(LargeArgs);
+extern template __global__ void socp_large_kernel<true, true>(LargeArgs);
 }  // namespace lg
 
-const void* large_kernel_ptr(bool xi) {
-  return xi ? (const void*)&lg::socp_large_kernel<true> : (const void*)&lg::socp_large_kernel<false>;
+const void* large_kernel_ptr(bool xi, bool gv) {
+  if (gv) return xi ? (const void*)&lg::socp_large_kernel<true, true> : (const void*)&lg::socp_large_kernel<false, true>;
+  return xi ? (const void*)&lg::socp_large_kernel<true, false> : (const void*)&lg::socp_large_kernel<false, false>;
 }
-const char* large_kernel_name(bool xi) { return xi ? "socp_large_xi_kernel" : "socp_large_kernel"; }
+const char* large_kernel_name(bool xi, bool gv) {
+  if (gv) return xi ? "socp_large_xi_gv_kernel" : "socp_large_gv_kernel";
+  return xi ? "socp_large_xi_kernel" : "socp_large_kernel";
+}
+#endif
 
 }  // namespace socp

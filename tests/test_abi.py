@@ -46,9 +46,12 @@ def test_supported_dims():
         cfg = CONFIGS[name]
         d = _lib.Dims(cfg.batch, cfg.n, cfg.m, cfg.k, len(cfg.cones))
         assert bool(L.socp_supported(C.byref(d))) == ok, name
-    # beyond the blocked kernel: n > 512, or k-vectors over the 160 KiB LDS
-    for n, m, k, nc in ((600, 0, 601, 1), (512, 64, 1000, 8)):
+    # beyond the blocked kernel: n > 512, m > 512, or more than 64 cones
+    for n, m, k, nc in ((600, 0, 601, 1), (64, 600, 128, 1), (256, 0, 130, 65)):
         assert not L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
+    # k-vectors over the 160 KiB LDS run with the vectors in HBM (the GV kernels)
+    for n, m, k, nc in ((512, 64, 1000, 8), (64, 16, 4096, 4)):
+        assert L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
 
 
 def test_null_context_is_an_api_error():

@@ -144,6 +144,32 @@ def test_c4_trajectory(oracle):
         assert_trajectory(cfg, g, r, B, 1e-8, K)
 
 
+WIDE = dict(n=512, m=64, k=1000, cones=[(1, 125 * i, 125) for i in range(8)], seed=0x534F4350 + 11)
+
+
+def test_wide_k_global_vector_kernel(oracle):
+    """(n, m, k) = (512, 64, 1000), 8 SOC(125): the problem's vectors (over
+    200 KiB) exceed a CU's LDS, so the blocked kernel keeps them in its HBM
+    workspace slot (socp_large_gv_kernel; densesolver.jl:19-38 allocates for
+    any size).  First iterations vs the oracle in the kernel's operation order
+    (X = W^-1 G, Cholesky + triangular solves) at 1e-8, 2 problems; and the
+    explicit-inverse build (SOCP_F_EXPLICIT_INVERSE) vs the structured oracle."""
+    from types import SimpleNamespace
+    cfg = SimpleNamespace(**WIDE)
+    B = 2
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    for K in (1, 2):
+        r = oracle_run(oracle, cfg, d, params=oracle.Params(maxit=K, tol=0.0,
+                                                            flags=oracle.F_STRUCTURED | oracle.F_CHOLSOLVE))
+        g = run(cfg, d, maxit=K, tol=0.0)
+        assert S.default_context().last_kernel_name() == "socp_large_gv_kernel"
+        assert_trajectory(cfg, g, r, B, 1e-8, K)
+    r = oracle_run(oracle, cfg, d, params=oracle.Params(maxit=1, tol=0.0, flags=oracle.F_STRUCTURED))
+    g = run(cfg, d, maxit=1, tol=0.0, explicit_inverse=True)
+    assert S.default_context().last_kernel_name() == "socp_large_xi_gv_kernel"
+    assert_trajectory(cfg, g, r, B, 1e-8, "xi")
+
+
 def test_c4_trajectory_k1_to_k5_fixture():
     """C4 at its bench K: the 4 committed oracle trajectories (tests/golden/
     trajectories.json, cases C4#0..3) solved as one batch for K = 1..5.  kappa_2(H)
