@@ -271,7 +271,9 @@ int socp_sqr_scaling(socp_sqr* h, double* l, double* wbs, double* mu);
  * every later launch).  c (B x n), b (B x m), h (B x k) in; x, y, z, s, iters,
  * status, res (B x 3: ||rd||, ||rp||, z's at the returned iterate; may be
  * NULL) out.  params NULL: socp_params_default.  Host or device pointers as
- * the handle's flags.  Afterwards the records hold the last factorisation. */
+ * the handle's flags.  Afterwards the records hold the last factorisation.
+ * With tol > 0 the call synchronises its stream every 4 iterations to stop
+ * launching once every problem has stopped (converged or failed). */
 int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b, const double* hvec,
                         const socp_params* params, double* x, double* y, double* z, double* s,
                         int32_t* iters, int32_t* status, double* res);

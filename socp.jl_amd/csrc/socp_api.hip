@@ -1036,7 +1036,7 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
   h->h2d_bytes = 0;
   // device block: c b h | x y z s | dx dy dz ds | rx ry rz rs | res | status iters active st_setup st_solve
   const size_t nd = (size_t)B * (n + m + k) + 4 * (size_t)B * (n + m + 2 * k) + 3 * (size_t)B;
-  const size_t ni = 5 * (size_t)B;
+  const size_t ni = 5 * (size_t)B + 1;
   typedef socp_sqr Q;
   if (h->buf[Q::Q_IPM].ensure(nd * sizeof(double) + ni * sizeof(int32_t)))
     return fail(SOCP_E_NOMEM, "device allocation failed");
@@ -1063,6 +1063,12 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
   int32_t* ip = (int32_t*)q;
   ia.status = ip; ia.iters = ip + B; ia.active = ip + 2 * B; ia.st_setup = ip + 3 * B;
   int32_t* st_solve = ip + 4 * B;
+  ia.n_active = ip + 5 * B;
+  {
+    const int32_t nb = (int32_t)B;
+    HIPCHK(hipMemcpyAsync(ia.n_active, &nb, sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));  // nb is a stack value
+  }
   const bool dev = h->dev;
   if (dev) {
     ia.c = c; ia.b = m ? b : nullptr; ia.h = hv;
@@ -1106,6 +1112,14 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
     TRY(ipm(3, it));                       // step, sigma, mu, corrector right-hand side
     TRY(sqr_launch(h, sv, false, false));  // solve_kkt (combined)
     TRY(ipm(4, it));                // step and update
+    // under a stopping rule, look every 4 iterations whether any problem is
+    // still iterating: the launches over an all-stopped batch are skipped
+    if (P.tol > 0.0 && (it & 3) == 3 && it + 1 < P.maxit) {
+      int32_t left = 0;
+      HIPCHK(hipMemcpyAsync(&left, ia.n_active, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      if (left <= 0) break;
+    }
   }
   if (res) TRY(ipm(5, 0));
   HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));

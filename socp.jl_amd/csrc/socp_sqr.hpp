@@ -119,6 +119,7 @@ struct SqrIpmArgs {
   int64_t rec_stride, r_l, r_wb, r_mu;
   double *x, *y, *z, *s, *dx, *dy, *dz, *ds, *rx, *ry, *rz, *rs, *res;
   int32_t *status, *iters, *active, *st_setup;
+  int32_t* n_active;  // problems still iterating (decremented where active[p] is cleared)
   double tol, step, init_eps;
 };
 size_t sqr_ipm_lds_bytes(int n, int m, int k);

@@ -146,34 +146,80 @@ __device__ __forceinline__ double e_of(const ConeTable& C, int i) {
 }
 
 // rd = A'y + G'z + c (into rdv, n), rp = Ax - b (m), rz = Gx + s - h (k); returns
-// (||rd||, ||rp||, z's) -- solver.jl:109-118, 122
+// (||rd||, ||rp||, z's) -- solver.jl:109-118, 122.
+// One pass over the columns of G and A (column-major: a column is contiguous,
+// so a lane per row reads coalesced), 16 columns at a time: every lane keeps
+// its rows' G x and A x running sums, and its share of the column dot
+// products G'z + A'y, which a reduce-scatter over the 16 lanes of a row and a
+// sum over the four rows turn into the 16 columns' totals (lane cl of every
+// row holds column j0 + cl).  k, m <= 256 (SQR_KMAX): four rows per lane.
 __device__ void residuals_w(const SqrIpmArgs& a, int64_t p, double* rdv, double* rpv, double* rzv, double (&r3)[3],
                             int lane) {
   const int n = a.n, m = a.m, k = a.k;
   const double* G = a.G + p * (int64_t)k * n;
   const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
   const double *x = a.x + p * n, *y = a.y + p * m, *z = a.z + p * k, *s = a.s + p * k;
+  const int cl = lane & 15;
+  constexpr int R = 4;
+  double zr[R], yr[R], gx[R], ax[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = lane + 64 * r;
+    zr[r] = i < k ? z[i] : 0.0;
+    yr[r] = i < m ? y[i] : 0.0;
+    gx[r] = 0.0;
+    ax[r] = 0.0;
+  }
   double d2 = 0.0, p2 = 0.0, zs = 0.0;
-  for (int j = lane; j < n; j += 64) {  // a lane per column: G, A column-major
-    double a1 = 0.0, a2 = 0.0;
-    for (int i = 0; i < m; ++i) a1 += A[(int64_t)j * m + i] * y[i];
-    for (int i = 0; i < k; ++i) a2 += G[(int64_t)j * k + i] * z[i];
-    const double v = a1 + a2 + a.c[p * n + j];
-    rdv[j] = v;
-    d2 += v * v;
+  for (int j0 = 0; j0 < n; j0 += 16) {
+    double P[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int j = j0 + c;
+      double pc = 0.0;
+      if (j < n) {  // wave-uniform
+        const double xj = x[j];
+        const double* Gj = G + (int64_t)j * k;
+        const double* Aj = m ? A + (int64_t)j * m : nullptr;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int i = lane + 64 * r;
+          if (64 * r < k) {  // wave-uniform
+            const double gv = i < k ? Gj[i] : 0.0;
+            pc = fma(gv, zr[r], pc);
+            gx[r] = fma(gv, xj, gx[r]);
+          }
+          if (64 * r < m) {
+            const double av = i < m ? Aj[i] : 0.0;
+            pc = fma(av, yr[r], pc);
+            ax[r] = fma(av, xj, ax[r]);
+          }
+        }
+      }
+      P[c] = pc;
+    }
+    int base = 0;
+    rs16<16, 8>(P, cl, base);  // base == cl: this row's partial of column j0 + cl
+    const double tot = rows_sum(P[0]);
+    const int j = j0 + cl;
+    if (lane < 16 && j < n) {
+      const double v = tot + a.c[p * n + j];
+      rdv[j] = v;
+      d2 += v * v;
+    }
   }
-  for (int i = lane; i < m; i += 64) {  // a lane per row
-    double acc = 0.0;
-    for (int j = 0; j < n; ++j) acc += A[(int64_t)j * m + i] * x[j];
-    const double v = acc - a.b[p * m + i];
-    rpv[i] = v;
-    p2 += v * v;
-  }
-  for (int i = lane; i < k; i += 64) {
-    double acc = 0.0;
-    for (int j = 0; j < n; ++j) acc += G[(int64_t)j * k + i] * x[j];
-    if (rzv) rzv[i] = acc + s[i] - a.h[p * k + i];
-    zs += z[i] * s[i];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = lane + 64 * r;
+    if (i < m) {
+      const double v = ax[r] - a.b[p * m + i];
+      rpv[i] = v;
+      p2 += v * v;
+    }
+    if (i < k) {
+      if (rzv) rzv[i] = gx[r] + s[i] - a.h[p * k + i];
+      zs += z[i] * s[i];
+    }
   }
   r3[0] = sqrt(ws64(d2));
   r3[1] = sqrt(ws64(p2));
@@ -213,6 +259,7 @@ __global__ __launch_bounds__(64) void socp_sqr_ipm_shift_kernel(SqrIpmArgs a) {
     if (lane == 0) {
       a.status[p] = a.st_setup[p];
       a.active[p] = 0;
+      atomicSub(a.n_active, 1);  // the host stops launching once none is left
     }
     return;
   }
@@ -245,6 +292,7 @@ __global__ __launch_bounds__(64) void socp_sqr_ipm_resid_kernel(SqrIpmArgs a) {
     if (lane == 0) {
       a.status[p] = SQR_DOMAIN;
       a.active[p] = 0;
+      atomicSub(a.n_active, 1);  // the host stops launching once none is left
     }
     return;
   }
@@ -263,6 +311,7 @@ __global__ __launch_bounds__(64) void socp_sqr_ipm_resid_kernel(SqrIpmArgs a) {
     if (lane == 0) {
       a.status[p] = 0;
       a.active[p] = 0;
+      atomicSub(a.n_active, 1);  // the host stops launching once none is left
     }
     return;
   }
@@ -270,6 +319,7 @@ __global__ __launch_bounds__(64) void socp_sqr_ipm_resid_kernel(SqrIpmArgs a) {
     if (lane == 0) {
       a.status[p] = st;
       a.active[p] = 0;
+      atomicSub(a.n_active, 1);  // the host stops launching once none is left
     }
     return;
   }
@@ -310,6 +360,7 @@ __global__ __launch_bounds__(64) void socp_sqr_ipm_step1_kernel(SqrIpmArgs a) {
     if (lane == 0) {
       a.status[p] = SQR_DOMAIN;
       a.active[p] = 0;
+      atomicSub(a.n_active, 1);  // the host stops launching once none is left
     }
     return;
   }
@@ -363,6 +414,7 @@ __global__ __launch_bounds__(64) void socp_sqr_ipm_step2_kernel(SqrIpmArgs a, in
     if (lane == 0) {
       a.status[p] = SQR_DOMAIN;
       a.active[p] = 0;
+      atomicSub(a.n_active, 1);  // the host stops launching once none is left
     }
     return;
   }
