@@ -273,7 +273,12 @@ int socp_sqr_scaling(socp_sqr* h, double* l, double* wbs, double* mu);
  * NULL) out.  params NULL: socp_params_default.  Host or device pointers as
  * the handle's flags.  Afterwards the records hold the last factorisation.
  * With tol > 0 the call synchronises its stream every 4 iterations to stop
- * launching once every problem has stopped (converged or failed). */
+ * launching once every problem has stopped (converged or failed).
+ * The initial point factors G'G (+ A'A where sing) with W = I: `sing` must be
+ * the flag Problem() computes (Socp.jl:49-56, cholesky(G'G) fails).  Where the
+ * given flag disagrees and that factorisation fails, the problem stops with
+ * status SOCP_CHOL_H_FAILED at iteration 0 -- the reference's sparse `\`
+ * (solver.jl:84) would solve the full KKT system instead. */
 int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b, const double* hvec,
                         const socp_params* params, double* x, double* y, double* z, double* s,
                         int32_t* iters, int32_t* status, double* res);
