@@ -1975,16 +1975,16 @@ struct Small {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] += row_partner<1>(v[r]);
   }
-  // out = L^-1 v: t_P = W_P (v_P - sum_{Q<P} L_PQ t_Q)
-  __device__ __forceinline__ void trsv_fwd(int vin, int vout) {
+  // out = L^-1 v: t_P = W_P (v_P - sum_{Q<P} L_PQ t_Q).  rc: v in column
+  // layout (every lane holds v[16i+cl]); tv: t in row layout (tv[P][r] =
+  // t[16P+g+4r] in every lane of row group g), for a product that takes its
+  // operand in that layout without the LDS round trip.
+  __device__ __forceinline__ void trsv_fwd_r(const double (&rc)[NQ], int vout, double (&tv)[NQ][4]) {
     MARK_BEGIN("trsv_fwd");
     LANE_IDS();
-    double rc[NQ], pa[NQ];  // v (column layout), lane partials of sum_Q L_iQ t_Q
+    double pa[NQ];  // lane partials of sum_Q L_iQ t_Q
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      rc[i] = LDS(vin + 16 * i + cl);
-      pa[i] = 0.0;
-    }
+    for (int i = 0; i < NQ; ++i) pa[i] = 0.0;
 #pragma unroll
     for (int P = 0; P < NQ; ++P) {
       const double rp = P > 0 ? rc[P] - rows_sum(pa[P]) : rc[P];
@@ -1997,14 +1997,17 @@ struct Small {
 #pragma unroll
         for (int r = 0; r < 4; ++r) pa[i] = fma(T[tri(i, P)][r], t4[r], pa[i]);
       if (cl < 4) LDS(vout + 16 * P + g + 4 * cl) = cl == 0 ? t4[0] : (cl == 1 ? t4[1] : (cl == 2 ? t4[2] : t4[3]));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tv[P][r] = t4[r];
     }
     SYNC();
   }
-  // out = L^-T v: x_P = W_P' (v_P - sum_{i>P} L_iP' x_i); in place is allowed
-  __device__ __forceinline__ void trsv_bwd(int vin, int vout) {
+  // out = L^-T v: x_P = W_P' (v_P - sum_{i>P} L_iP' x_i); in place is allowed.
+  // xs: x in column layout (every lane holds x[16P+cl]).
+  __device__ __forceinline__ void trsv_bwd(int vin, int vout, double (&xs)[NQ]) {
     MARK_BEGIN("trsv_bwd");
     LANE_IDS();
-    double ur[NQ][4], pa[NQ][4], xs[NQ];  // v (row layout), lane partials of sum_i L_iP' x_i
+    double ur[NQ][4], pa[NQ][4];  // v (row layout), lane partials of sum_i L_iP' x_i
 #pragma unroll
     for (int P = 0; P < NQ; ++P)
 #pragma unroll
@@ -2076,6 +2079,12 @@ struct Small {
     gemv_G_chunk<0, (NP < 8 ? NP : 8)>(uq, add1, add2, out);
     SYNC();
   }
+  // the same with u in column layout in registers (uq[q] = u[16q+cl])
+  __device__ __forceinline__ void gemv_G_r(const double (&uq)[NQ], int add1, int add2, int out) {
+    MARK_BEGIN("gemv_G");
+    gemv_G_chunk<0, (NP < 8 ? NP : 8)>(uq, add1, add2, out);
+    SYNC();
+  }
 
   // gemv_G and gemv_Gt in one pass over G (the residuals' Gx and G'z): each
   // G element is copied out of its AGPRs once for both products; the
@@ -2135,18 +2144,37 @@ struct Small {
     }
   }
 
+#ifndef SOCP_LDS_BATCH
+#define SOCP_LDS_BATCH 8  // LDS reads issued per round trip in the A products
+#endif
+  static constexpr int AMB = (NQ * 4) % SOCP_LDS_BATCH == 0 ? SOCP_LDS_BATCH : 4;
+  static constexpr int ATB = (MQ * 4) % (SOCP_LDS_BATCH / NQ > 0 ? SOCP_LDS_BATCH / NQ : 1) == 0
+                                 ? (SOCP_LDS_BATCH / NQ > 0 ? SOCP_LDS_BATCH / NQ : 1)
+                                 : 1;
   // acc[q] (all lanes) = (A' v)[16q+cl]: rows split over the 4 lane groups
   __device__ __forceinline__ void At_mv(int v, double (&acc)[NQ], int base = O_A) {
     MARK_BEGIN("At_mv");
     LANE_IDS();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+    // the reads of a step batch issued before its products (one LDS round
+    // trip per SOCP_LDS_BATCH rows, not one per row: the scheduler otherwise
+    // interleaves read, wait, fma)
 #pragma unroll
-    for (int s = 0; s < MQ * 4; ++s) {
-      const int i = g + 4 * s;
-      const double vi = LDS(v + i);
+    for (int s0 = 0; s0 < MQ * 4; s0 += ATB) {
+      double vi[ATB], av[ATB][NQ];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc[q] = fma(LDS(base + i * LDA + 16 * q + cl), vi, acc[q]);
+      for (int s = 0; s < ATB; ++s) {
+        const int i = g + 4 * (s0 + s);
+        vi[s] = LDS(v + i);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) av[s][q] = LDS(base + i * LDA + 16 * q + cl);
+      }
+      SCHED_FENCE();
+#pragma unroll
+      for (int s = 0; s < ATB; ++s)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] = fma(av[s][q], vi[s], acc[q]);
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -2164,7 +2192,46 @@ struct Small {
       const int i = 16 * tm + cl;
       double acc = 0.0;
 #pragma unroll
-      for (int t = 0; t < NQ * 4; ++t) acc = fma(LDS(base + i * LDA + g + 4 * t), LDS(u + g + 4 * t), acc);
+      for (int t0 = 0; t0 < NQ * 4; t0 += AMB) {
+        double av[AMB], uv[AMB];
+#pragma unroll
+        for (int t = 0; t < AMB; ++t) {
+          av[t] = LDS(base + i * LDA + g + 4 * (t0 + t));
+          uv[t] = LDS(u + g + 4 * (t0 + t));
+        }
+        SCHED_FENCE();
+#pragma unroll
+        for (int t = 0; t < AMB; ++t) acc = fma(av[t], uv[t], acc);
+      }
+      acc = rows_sum(acc);
+      if (g == 0 && i < m) {
+        const double v = acc - LDS(sub + i);
+        LDS(out + i) = v;
+        sq = fma(v, v, sq);
+      }
+    }
+    return sq;
+  }
+
+  // A_mv with u in row layout in registers (tv[P][r] = u[16P+g+4r], trsv_fwd_r's
+  // output): the same products in the same order
+  __device__ __forceinline__ double A_mv_r(const double (&tv)[NQ][4], int sub, int out, int base) {
+    MARK_BEGIN("A_mv");
+    LANE_IDS();
+    double sq = 0.0;
+#pragma unroll
+    for (int tm = 0; tm < MQ; ++tm) {
+      const int i = 16 * tm + cl;
+      double acc = 0.0;
+#pragma unroll
+      for (int t0 = 0; t0 < NQ * 4; t0 += AMB) {
+        double av[AMB];
+#pragma unroll
+        for (int t = 0; t < AMB; ++t) av[t] = LDS(base + i * LDA + g + 4 * (t0 + t));
+        SCHED_FENCE();
+#pragma unroll
+        for (int t = 0; t < AMB; ++t) acc = fma(av[t], tv[(t0 + t) >> 2][(t0 + t) & 3], acc);
+      }
       acc = rows_sum(acc);
       if (g == 0 && i < m) {
         const double v = acc - LDS(sub + i);
@@ -2244,6 +2311,9 @@ struct Small {
   __device__ __forceinline__ void solve_matrix_part(bool init) {
     MARK_BEGIN("solve_matrix_part");
     LANE_IDS();
+    // n0 in column layout, in every lane (the CHOL path hands it to trsv_fwd_r
+    // in registers; the sweep path's symv reads it from N0)
+    double n0[NQ];
     {
       double acc[NQ], at[NQ];
       if (SOCP_KO & 512) {
@@ -2252,24 +2322,31 @@ struct Small {
         gemv_Gt(T2, acc);
       }
       if (sing) At_mv(RP, at);
-      if (g == 0) {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const int j = 16 * q + cl;
-          double v = acc[q] + LDS(RD + j);
-          if (sing) v = v + at[q];
-          LDS(N0 + j) = v;
-        }
+      for (int q = 0; q < NQ; ++q) {
+        const int j = 16 * q + cl;
+        double v = acc[q] + LDS(RD + j);
+        if (sing) v = v + at[q];
+        n0[q] = v;
+      }
+      if (!CHOL && g == 0) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) LDS(N0 + 16 * q + cl) = n0[q];
       }
     }
-    SYNC();
+    if constexpr (!CHOL) SYNC();
     STAMP_X(4);
+    double tv[NQ][4];  // t = L^-1 n0 in row layout (CHOL)
+    double cxr[NQ];    // cx in column layout (CHOL: trsv_bwd's output)
     if constexpr (CHOL) {
       if (SOCP_KO & 256) {
-        for (int j = lane; j < NPAD; j += 64) LDS(TN + j) = LDS(N0 + j);
+        if (g == 0)
+          for (int q = 0; q < NQ; ++q) LDS(TN + 16 * q + cl) = n0[q];
         SYNC();
+        for (int P = 0; P < NQ; ++P)
+          for (int r = 0; r < 4; ++r) tv[P][r] = LDS(TN + 16 * P + g + 4 * r);
       } else {
-        trsv_fwd(N0, TN);    // t = L^-1 n0
+        trsv_fwd_r(n0, TN, tv);  // t = L^-1 n0
       }
     } else
       symv<NQ>(T, N0, TN);   // Li n0
@@ -2277,7 +2354,7 @@ struct Small {
     if (SOCP_KO & 2048) {
       for (int j = lane; j < m; j += 64) LDS(M0 + j) = LDS(TN + j);
     } else if constexpr (CHOL)
-      A_mv(TN, RP, M0, O_AL);  // m0 = A Li n0 - dy = Z't - dy
+      A_mv_r(tv, RP, M0, O_AL);  // m0 = A Li n0 - dy = Z't - dy
     else if constexpr (AL_LDS)
       A_mv(N0, RP, M0, O_AL);  // m0 = (A Li) n0 - dy: no wait for Li n0
     else
@@ -2310,7 +2387,12 @@ struct Small {
       }
       SYNC();
       if constexpr (CHOL) {
-        if (!(SOCP_KO & 256)) trsv_bwd(RX, RX);
+        if (!(SOCP_KO & 256)) {
+          trsv_bwd(RX, RX, cxr);
+        } else {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) cxr[q] = LDS(RX + 16 * q + cl);
+        }
       }
       STAMP_X(7);
     } else {
@@ -2326,6 +2408,8 @@ struct Small {
     if (SOCP_KO & 1024) {
       for (int i = lane; i < k; i += 64) LDS(K1 + i) = LDS(RX + (i & 63)) - LDS(K2 + i);
       SYNC();
+    } else if constexpr (CHOL) {
+      gemv_G_r(cxr, -1, K2, K1);  // cx from trsv_bwd's registers
     } else {
       gemv_G(RX, -1, K2, K1);
     }
