@@ -426,6 +426,17 @@ __device__ __forceinline__ void rs16(double* P, int cl, int& base) {
     rs16<C, M / 2>(P, cl, base);
   }
 }
+// the lane's first entry index after rs16<C, M> (its `base`), known up front
+template <int C, int M>
+__device__ __forceinline__ int rs16_base(int cl) {
+  if constexpr (M == 0) {
+    return 0;
+  } else if constexpr (C % 2 == 0) {
+    return ((cl & M) != 0 ? C / 2 : 0) + rs16_base<C / 2, M / 2>(cl);
+  } else {
+    return rs16_base<C, M / 2>(cl);
+  }
+}
 template <int C, int M>
 struct RSCount {
   static constexpr int value =
@@ -639,6 +650,11 @@ struct Small {
   // waves per SIMD: C1's <2, 12, 1> takes 209 + 48 registers with them, 208 + 48
   // without
   static constexpr bool TILE_INPL = SOCP_TILE_INPLACE != 0 && NQ * NP > 24;
+  // the solves' per-cone constants read ahead of the cone reductions (their
+  // latency under the DPP chains) where registers allow: not in the kernels
+  // that keep two waves per SIMD (C1's <2, 12, 1> would take 217 + 48; every
+  // NQ = 1 shape)
+  static constexpr bool HOIST_CST = NQ * NP > 24 && NQ > 1;
   static constexpr int C_ = SH::nv(NV_C), X_ = SH::nv(NV_X), RD = SH::nv(NV_RD),
                        RX = SH::nv(NV_RX), N0 = SH::nv(NV_N0), TN = SH::nv(NV_TN);
   static constexpr int B_ = SH::mv(MV_B), Y_ = SH::mv(MV_Y), RP = SH::mv(MV_RP),
@@ -691,6 +707,10 @@ struct Small {
       LDS(O_COFF + lane) = a.cones.offs[lane];
       LDS(O_CDIM + lane) = a.cones.dim[lane];
       LDS(O_CKIND + lane) = a.cones.kind[lane];
+      if constexpr (HOIST_CST) {
+        lc_soc = a.cones.kind[lane] == SOC_K;
+        lc_off = a.cones.offs[lane];
+      }
     }
     for (int i = lane; i < KP; i += 64) {
       int code = 3;
@@ -736,6 +756,10 @@ struct Small {
                    // 2 no residuals, 4 no compute_U, 8 no S factorisation
 #endif
   bool ko_gloaded = false;
+  // lane c < nc: its cone's kind and offset (per-cone work without the table
+  // round trips)
+  bool lc_soc = false;
+  int lc_off = 0;
   __device__ __forceinline__ void load_problem(int64_t p) {
     MARK_BEGIN("load_problem");
     LANE_IDS();
@@ -966,8 +990,11 @@ struct Small {
 
   // max over cones of the value the first lane of every cone stored at O_TOTC + off
   __device__ __forceinline__ double cone_max(int off) const {
-    double t = -INFINITY;
-    for (int c = 0; c < nc; ++c) t = fmax(t, LDS(O_TOTC + off + c));
+    double t = -INFINITY, v[NCS];  // all reads in one round trip (the entries c >= nc are not used)
+#pragma unroll
+    for (int c = 0; c < NCS; ++c) v[c] = LDS(O_TOTC + off + c);
+#pragma unroll
+    for (int c = 0; c < NCS; ++c) t = c < nc ? fmax(t, v[c]) : t;
     return t;
   }
 
@@ -1004,8 +1031,8 @@ struct Small {
     MARK_BEGIN("scal_cone1");
     bool dm = false;
     // ---- cone lanes: the SOC branch of compute_scaling (scalings.jl:32-99)
-    if (lane < nc && (int)LDS(O_CKIND + lane) == SOC_K) {
-      const int c = lane, o = (int)LDS(O_COFF + c);
+    if (HOIST_CST ? lc_soc : (lane < nc && (int)LDS(O_CKIND + lane) == SOC_K)) {
+      const int c = lane, o = HOIST_CST ? lc_off : (int)LDS(O_COFF + c);
       const double z0 = LDS(Z_ + o), s0 = LDS(S_ + o);
       const double onrmz = z0 * z0 - cone_tot(0, c), onrms = s0 * s0 - cone_tot(1, c);
       const double nrmz = sqrt(onrmz), nrms = sqrt(onrms);
@@ -1075,8 +1102,8 @@ struct Small {
     if (lane < nc) {
       const int c = lane;
       const double l1 = cone_tot(0, c);
-      if ((int)LDS(O_CKIND + c) == SOC_K) {
-        const int o = (int)LDS(O_COFF + c);
+      if (HOIST_CST ? lc_soc : (int)LDS(O_CKIND + c) == SOC_K) {
+        const int o = HOIST_CST ? lc_off : (int)LDS(O_COFF + c);
         const double l0 = LDS(cc(CC_L0, c));
         const double aa = l0 * l0 - l1;
         da = aa < 0.0;
@@ -1129,6 +1156,28 @@ struct Small {
       v[s][1] = tail ? wb[s] * x[s] : 0.0;
       v[s][2] = tail ? wb[s] * dz[s] : 0.0;
     }
+    // the scaling's per-cone constants and the element coefficients are read
+    // before the reduction: their LDS latency hides under its DPP chain
+    double cst[2][12];
+    auto read_cst = [&]() {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane, c = ci[s];
+      cst[s][0] = ccv(CC_L0, c);
+      cst[s][1] = ccv(CC_IAA, c);
+      cst[s][2] = ccv(CC_IL0, c);
+      cst[s][3] = ccv(CC_IL0AA, c);
+      cst[s][4] = ccv(CC_MU, c);
+      cst[s][5] = ccv(CC_IMU, c);
+      cst[s][6] = ccv(CC_WB0, c);
+      cst[s][7] = ccv(CC_I1, c);
+      cst[s][8] = ccv(CC_W2, c);
+      cst[s][9] = ccv(CC_WL, c);
+      cst[s][10] = LDS(IL + i);
+      cst[s][11] = LDS(CA + i);
+    }
+    };
+    if constexpr (HOIST_CST) read_cst();
     cone_reduce<3, 0>(v);
     STAMP_X(8);
     MARK_BEGIN("head_post");
@@ -1136,9 +1185,12 @@ struct Small {
     for (int s = 0; s < 2; ++s) {
       const int i = 64 * s + lane, c = ci[s];
       const double t = v[s][0], u = v[s][1], w = v[s][2];
-      const double l0 = ccv(CC_L0, c), iaa = ccv(CC_IAA, c), il0 = ccv(CC_IL0, c), il0aa = ccv(CC_IL0AA, c);
-      const double mu = ccv(CC_MU, c), imu = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
-      const double w2 = ccv(CC_W2, c), wl = ccv(CC_WL, c);
+#define CST(j, expr) (HOIST_CST ? cst[s][j] : (expr))
+      const double l0 = CST(0, ccv(CC_L0, c)), iaa = CST(1, ccv(CC_IAA, c)), il0 = CST(2, ccv(CC_IL0, c)),
+                   il0aa = CST(3, ccv(CC_IL0AA, c));
+      const double mu = CST(4, ccv(CC_MU, c)), imu = CST(5, ccv(CC_IMU, c)), wb0 = CST(6, ccv(CC_WB0, c)),
+                   i1 = CST(7, ccv(CC_I1, c));
+      const double w2 = CST(8, ccv(CC_W2, c)), wl = CST(9, ccv(CC_WL, c));
       // iprod! (vectors.jl:105-125)
       const double k00 = (x0[s] * l0 - t) * iaa;
       const double k0t = -(x0[s] * lam[s] * iaa) + x[s] * il0 + lam[s] * t * il0aa;
@@ -1153,9 +1205,9 @@ struct Small {
       const double y0 = imu * (wb0 * k20 - a1);
       const double a2 = imu * (a1 + cy * w2);
       // POC: elementwise, with 1/lambda and 1/w = CA
-      const double k0p = x[s] * LDS(IL + i);
+      const double k0p = x[s] * CST(10, LDS(IL + i));
       const double k2p = dz[s] - wb[s] * k0p;
-      const double ca = LDS(CA + i);
+      const double ca = CST(11, LDS(CA + i));
       const bool poc = kd[s] == 0, hd = kd[s] == 1;
       const double k0 = poc ? k0p : (hd ? k00 : k0t);
       const double k2 = poc ? k2p : dz[s] - (hd ? k10 : k1t);
@@ -1199,6 +1251,26 @@ struct Small {
       v[s][1] = tail ? lam[s] * k1[s] : 0.0;
       v[s][2] = tail ? lam[s] * k0[s] : 0.0;
     }
+    double cst[2][12];  // read before the reduction (as in solve_head)
+    auto read_cst = [&]() {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane, c = ci[s];
+      cst[s][0] = ccv(CC_MU, c);
+      cst[s][1] = ccv(CC_IMU, c);
+      cst[s][2] = ccv(CC_WB0, c);
+      cst[s][3] = ccv(CC_I1, c);
+      cst[s][4] = ccv(CC_W2, c);
+      cst[s][5] = ccv(CC_WL, c);
+      cst[s][6] = LDS(CA + i);
+      cst[s][7] = ccv(CC_DLT, c);
+      cst[s][8] = ccv(CC_SA, c);
+      cst[s][9] = ccv(CC_L0, c);
+      cst[s][10] = ccv(CC_SAL, c);
+      cst[s][11] = LDS(IL + i);
+    }
+    };
+    if constexpr (HOIST_CST) read_cst();
     cone_reduce<3, 0>(v);
     STAMP_X(9);
     MARK_BEGIN("tail_post1");
@@ -1207,9 +1279,10 @@ struct Small {
     for (int s = 0; s < 2; ++s) {
       const int i = 64 * s + lane, c = ci[s];
       const double a1 = v[s][0];
-      const double mu = ccv(CC_MU, c), imu = ccv(CC_IMU, c), wb0 = ccv(CC_WB0, c), i1 = ccv(CC_I1, c);
-      const double w2 = ccv(CC_W2, c), wl = ccv(CC_WL, c);
-      const double ca = LDS(CA + i);
+      const double mu = CST(0, ccv(CC_MU, c)), imu = CST(1, ccv(CC_IMU, c)), wb0 = CST(2, ccv(CC_WB0, c)),
+                   i1 = CST(3, ccv(CC_I1, c));
+      const double w2 = CST(4, ccv(CC_W2, c)), wl = CST(5, ccv(CC_WL, c));
+      const double ca = CST(6, LDS(CA + i));
       const bool poc = kd[s] == 0, hd = kd[s] == 1;
       const double cy = a1 * i1 - k10[s];
       const double y0 = imu * (wb0 * k10[s] - a1);
@@ -1219,7 +1292,7 @@ struct Small {
       y0v[s] = y0;
       kn[s] = k0[s] - y[s];
       kn0[s] = k00[s] - y0;
-      const double del = ccv(CC_DLT, c) - a2;  // wbar_1'kn_1
+      const double del = CST(7, ccv(CC_DLT, c)) - a2;  // wbar_1'kn_1
       const double cs = poc ? wb[s] * kn[s]
                             : (hd ? mu * (wb0 * kn0[s] + del) : mu * (kn[s] + (kn0[s] + del * i1) * wb[s]));
       ly[s] = imu * (v[s][1] + cy * wl);  // lambda_1'y_1
@@ -1243,12 +1316,12 @@ struct Small {
         LDS(K0 + i) = kn[s];
       }
       const bool tail = kd[s] == 2, poc = kd[s] == 0, real = kd[s] != 3;
-      const double sa = ccv(CC_SA, c), l0 = ccv(CC_L0, c), sal = ccv(CC_SAL, c);
+      const double sa = CST(8, ccv(CC_SA, c)), l0 = CST(9, ccv(CC_L0, c)), sal = CST(10, ccv(CC_SAL, c));
       r1y[s] = sa * l0 * y0v[s] - sa * ly[s];
       r1k[s] = sa * l0 * kn0[s] - sa * lkn[s];
       const double cyy = (r1y[s] + y0v[s]) * sal, cyk = (r1k[s] + kn0[s]) * sal;
       const double qy = sa * (y[s] - cyy * sa * lam[s]), qk = sa * (kn[s] - cyk * sa * lam[s]);
-      const double il = LDS(IL + i);
+      const double il = CST(11, LDS(IL + i));
       w[s][0] = tail ? qy * qy : 0.0;
       w[s][1] = tail ? qk * qk : 0.0;
       w[s][2] = poc ? -y[s] * il : -INFINITY;
@@ -1262,7 +1335,8 @@ struct Small {
     for (int s = 0; s < 2; ++s) {
       const int c = ci[s];
       if (64 * s >= k || kd[s] == 3 || 64 * s + lane != eo[s]) continue;
-      const double sa = ccv(CC_SA, c);
+      const double sa = CST(8, ccv(CC_SA, c));
+#undef CST
       const double vy = sqrt(w[s][0]) - sa * r1y[s];
       const double vk = sqrt(w[s][1]) - sa * r1k[s];
       LDS(O_TOTC + c) = kd[s] == 0 ? fmax(w[s][2], w[s][3]) : fmax(vy, vk);
@@ -1281,8 +1355,11 @@ struct Small {
   __device__ __forceinline__ void affine_post(double tstep, double ll) {
     MARK_BEGIN("affine_post");
     LANE_IDS();
-    double kk = 0.0;
-    for (int c = 0; c < nc; ++c) kk += LDS(cc(CC_KK, c));
+    double kk = 0.0, kv[NCS];  // one round trip
+#pragma unroll
+    for (int c = 0; c < NCS; ++c) kv[c] = LDS(cc(CC_KK, c));
+#pragma unroll
+    for (int c = 0; c < NCS; ++c) kk = c < nc ? kk + kv[c] : kk;
     const double t = tstep;
     const double rho = 1.0 - t - t * t * kk / ll;
     const double cr = isnan(rho) ? rho : (rho < 0.0 ? 0.0 : (rho > 1.0 ? 1.0 : rho));
@@ -1290,20 +1367,49 @@ struct Small {
     const double mu_ipm = ll / a.deg;
     const double scf = 1.0 - sig;
     const double smu = sig * mu_ipm;
+    if constexpr (HOIST_CST) {
+      // every read first (one round trip; n, m <= 64 here), then the updates
+      double a2[2], a3[2], a20[2], a30[2], kkc[2], dsv[2], dzv[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int i = 64 * s + lane;
-      if (kd[s] == 3) continue;
-      const double a2 = LDS(K0 + i), a3 = LDS(T1 + i);
-      const double a20 = LDS(K0 + eo[s]), a30 = LDS(T1 + eo[s]);
-      const double kt1 = kd[s] == 0 ? a2 * a3 : (kd[s] == 1 ? LDS(cc(CC_KK, ci[s])) : a20 * a3 + a30 * a2);
-      const double e = kd[s] == 2 ? 0.0 : 1.0;
-      LDS(DS + i) = LDS(DS + i) + (smu * e - kt1);
-      LDS(DZ + i) = LDS(DZ + i) * scf;
+      for (int s = 0; s < 2; ++s) {
+        const int i = 64 * s + lane;
+        a2[s] = LDS(K0 + i);
+        a3[s] = LDS(T1 + i);
+        a20[s] = LDS(K0 + eo[s]);
+        a30[s] = LDS(T1 + eo[s]);
+        kkc[s] = LDS(cc(CC_KK, ci[s]));
+        dsv[s] = LDS(DS + i);
+        dzv[s] = LDS(DZ + i);
+      }
+      const double rdv = LDS(RD + lane), rpv = LDS(RP + (lane < MPAD ? lane : 0));
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int i = 64 * s + lane;
+        if (kd[s] == 3) continue;
+        const double kt1 = kd[s] == 0 ? a2[s] * a3[s] : (kd[s] == 1 ? kkc[s] : a20[s] * a3[s] + a30[s] * a2[s]);
+        const double e = kd[s] == 2 ? 0.0 : 1.0;
+        LDS(DS + i) = dsv[s] + (smu * e - kt1);
+        LDS(DZ + i) = dzv[s] * scf;
+      }
+      if (lane < n) LDS(RD + lane) = rdv * scf;
+      if (lane < m) LDS(RP + lane) = rpv * scf;
+      SYNC();
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int i = 64 * s + lane;
+        if (kd[s] == 3) continue;
+        const double a2 = LDS(K0 + i), a3 = LDS(T1 + i);
+        const double a20 = LDS(K0 + eo[s]), a30 = LDS(T1 + eo[s]);
+        const double kt1 = kd[s] == 0 ? a2 * a3 : (kd[s] == 1 ? LDS(cc(CC_KK, ci[s])) : a20 * a3 + a30 * a2);
+        const double e = kd[s] == 2 ? 0.0 : 1.0;
+        LDS(DS + i) = LDS(DS + i) + (smu * e - kt1);
+        LDS(DZ + i) = LDS(DZ + i) * scf;
+      }
+      for (int j = lane; j < n; j += 64) LDS(RD + j) = LDS(RD + j) * scf;
+      for (int i = lane; i < m; i += 64) LDS(RP + i) = LDS(RP + i) * scf;
+      SYNC();
     }
-    for (int j = lane; j < n; j += 64) LDS(RD + j) = LDS(RD + j) * scf;
-    for (int i = lane; i < m; i += 64) LDS(RP + i) = LDS(RP + i) * scf;
-    SYNC();
   }
 
   // max_step(-iz), max_step(iz) (mats.jl:1-28) for the initial shift (solver.jl:88-101)
@@ -1342,10 +1448,17 @@ struct Small {
   __device__ __forceinline__ void compute_U() {
     MARK_BEGIN("compute_U");
     LANE_IDS();
+    // HOIST_CST shapes: every row's weight read once, in one round trip
+    double wall[HOIST_CST ? NP : 1];
+    if constexpr (HOIST_CST) {
+#pragma unroll
+      for (int pp = 0; pp < NP; ++pp) wall[pp] = LDS(WB + 4 * pp + g);
+    }
     for (int c = 0; c < nc; ++c) {
       if (a.cones.kind[c] != SOC_K) continue;
       const int o = a.cones.offs[c], d = a.cones.dim[c];
       const double hw = -(1.0 + LDS(WB + o));  // the head row's weight
+      const double inv = LDS(cc(CC_I1, c));
       const int p0 = o >> 2, p1 = (o + d + 3) >> 2;  // row steps [p0, p1) meet the cone
       double acc[NQ];
 #pragma unroll
@@ -1358,7 +1471,10 @@ struct Small {
 #pragma unroll
         for (int u = 0; u < U4; ++u) {
           const int row = 4 * (pb + u) + g;  // < KP: in the LDS k-vector
-          w[u] = (pb + u < NP) ? LDS(WB + row) : 0.0;
+          if constexpr (HOIST_CST)
+            w[u] = (pb + u < NP) ? wall[pb + u < NP ? pb + u : 0] : 0.0;
+          else
+            w[u] = (pb + u < NP) ? LDS(WB + row) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < U4; ++u) {
@@ -1374,7 +1490,6 @@ struct Small {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) acc[q] = rows_sum(acc[q]);
       if (g == 0) {
-        const double inv = LDS(cc(CC_I1, c));
 #pragma unroll
         for (int q = 0; q < NQ; ++q) LDS(O_U + c * NPAD + 16 * q + cl) = acc[q] * inv;
       }
@@ -1384,7 +1499,7 @@ struct Small {
 
   // ----------------------------------------------------- H = X'X (+A'A)
 #ifndef SOCP_SYRK_PIPE
-#define SOCP_SYRK_PIPE 1
+#define SOCP_SYRK_PIPE 2  // 2: row coefficients two steps ahead, U rows one step ahead
 #endif
 #ifndef SOCP_SYRK_M
 #define SOCP_SYRK_M 1
@@ -1400,12 +1515,70 @@ struct Small {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) X[q] = fma(cav, a_get(G[pp][q]), cbv * LDS(O_U + cid * NPAD + 16 * q + cl));
   }
+  // genX in two halves, for a two-deep pipeline: the row coefficients (and the
+  // cone id that addresses U) first, the U row and the products a step later
+  struct XCoef {
+    double ca, cb;
+    int ub;  // LDS index of the cone's U row + cl
+  };
+  __device__ __forceinline__ XCoef genX_a(int pp) {
+    LANE_IDS();
+    const int row = 4 * pp + g;
+    XCoef c;
+    c.ca = LDS(CA + row);
+    c.cb = LDS(CBV + row);
+    c.ub = O_U + (((int)LDS(O_RC + row)) >> 2) * NPAD + cl;
+    return c;
+  }
+  __device__ __forceinline__ void genX_b(int pp, const XCoef& c, double (&X)[NQ]) {
+    double u[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) u[q] = LDS(c.ub + 16 * q);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) X[q] = fma(c.ca, a_get(G[pp][q]), c.cb * u[q]);
+  }
   __device__ __forceinline__ void form_H(bool addAA) {
     MARK_BEGIN("form_H");
     LANE_IDS();
 #pragma unroll
     for (int t = 0; t < NT; ++t) T[t] = (d4){0.0, 0.0, 0.0, 0.0};
-#if SOCP_SYRK_PIPE
+#if SOCP_SYRK_PIPE == 2
+    double Xc[NQ];
+    XCoef c1;
+    {
+      const XCoef c0 = genX_a(0);
+      if (NP > 1) c1 = genX_a(1 < NP ? 1 : 0);
+      genX_b(0, c0, Xc);
+    }
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp) {
+      XCoef c2 = c1;
+      if (pp + 2 < NP) c2 = genX_a(pp + 2 < NP ? pp + 2 : 0);
+      double Xn[NQ];
+      if (pp + 1 < NP) genX_b(pp + 1 < NP ? pp + 1 : 0, c1, Xn);
+#pragma unroll
+      for (int ti = 0; ti < NQ; ++ti)
+#pragma unroll
+        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = CHOL ? mfma(Xc[tj], Xc[ti], T[tri(ti, tj)])
+                                                                : mfma(Xc[ti], Xc[tj], T[tri(ti, tj)]);
+      if (pp + 1 < NP) {
+        // the step's LDS reads behind the first MFMAs, its VALU after them
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+        for (int r = 2; r < NT; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, SOCP_SYRK_V, 0);
+        }
+      }
+      SCHED_FENCE();
+      c1 = c2;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) Xc[q] = Xn[q];
+    }
+#elif SOCP_SYRK_PIPE
     // software-pipelined: row step pp+1 of X is generated (LDS coefficient
     // reads, AGPR reads of G, FMAs) while the MFMAs of step pp run, one MFMA
     // between every few of those instructions
@@ -1938,9 +2111,9 @@ struct Small {
       P1row[ti] = P1[0] + 0.0 * base;
       // stash the row index in base via the lane's own cl bits (see write below)
     }
+    if constexpr (Q > 1) {
 #pragma unroll
-    for (int t = 0; t < Q; ++t) {
-      P2[t] = rows_sum(P2[t]);
+      for (int t = 0; t < Q; ++t) P2[t] = rows_sum(P2[t]);
     }
     SYNC();
     {
@@ -1951,11 +2124,30 @@ struct Small {
       for (int ti = 0; ti < Q; ++ti) LDS(vout + 16 * ti + g + 4 * r) = P1row[ti];
     }
     SYNC();
-    if (g == 0) {
+    if constexpr (Q > 1) {  // one tile has no strictly upper part
+      if (g == 0) {
 #pragma unroll
-      for (int t = 0; t < Q; ++t) LDS(vout + 16 * t + cl) += P2[t];
+        for (int t = 0; t < Q; ++t) LDS(vout + 16 * t + cl) += P2[t];
+      }
+      SYNC();
     }
-    SYNC();
+  }
+
+  // symv<1> with v in column layout in registers (vc = v[cl], every lane); out
+  // to LDS as symv's, and in registers in row layout, yr[s] = out[g + 4s]
+  __device__ __forceinline__ void symv1_r(const d4& M, double vc, int vout, double (&yr)[4]) {
+    MARK_BEGIN("symv");
+    LANE_IDS();
+    double P1[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) P1[r] = fma(M[r], vc, 0.0);
+    int base = 0;
+    rs16<4, 8>(P1, cl, base);  // row g + 4 (cl >> 2)
+    LDS(vout + g + 4 * (cl >> 2)) = P1[0];
+    yr[0] = dpp_all<0x150>(P1[0]);
+    yr[1] = dpp_all<0x154>(P1[0]);
+    yr[2] = dpp_all<0x158>(P1[0]);
+    yr[3] = dpp_all<0x15C>(P1[0]);
   }
 
   // Triangular solves against chol()'s factor (T[tri(P, P)] = W_P = L_PP^-1,
@@ -1965,7 +2157,23 @@ struct Small {
   // all-reduce; M'u (u[g+4r] in the lanes of row group g) gives (M'u)[cl]
   // after the four-row sum.  The off-diagonal products of earlier tiles are
   // accumulated lane-locally and reduced once per tile.
+#ifndef SOCP_ALLRED_RS
+#define SOCP_ALLRED_RS 1
+#endif
   __device__ __forceinline__ static void allred16(double (&v)[4]) {
+#if SOCP_ALLRED_RS
+    // reduce-scatter (entry r ends in lanes 4r..4r+3 of the row: rs16's base is
+    // cl >> 2), then each entry broadcast from lane 4r by row_newbcast: 9 DPP
+    // moves and 6 adds per 64-bit lane value instead of 16 and 16
+    LANE_IDS();
+    int base = 0;
+    rs16<4, 8>(v, cl, base);
+    const double t = v[0];
+    v[0] = dpp_all<0x150>(t);
+    v[1] = dpp_all<0x154>(t);
+    v[2] = dpp_all<0x158>(t);
+    v[3] = dpp_all<0x15C>(t);
+#else
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] += row_partner<8>(v[r]);
 #pragma unroll
@@ -1974,6 +2182,7 @@ struct Small {
     for (int r = 0; r < 4; ++r) v[r] += row_partner<2>(v[r]);
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] += row_partner<1>(v[r]);
+#endif
   }
   // out = L^-1 v: t_P = W_P (v_P - sum_{Q<P} L_PQ t_Q).  rc: v in column
   // layout (every lane holds v[16i+cl]); tv: t in row layout (tv[P][r] =
@@ -2044,6 +2253,18 @@ struct Small {
   template <int P0, int CH>
   __device__ __forceinline__ void gemv_G_chunk(const double (&uq)[NQ], int add1, int add2, int out) {
     LANE_IDS();
+    constexpr int CF = RSCount<CH, 8>::value;
+    // the addends of the rows this lane ends up holding, read before the products
+    double a1[CF], a2[CF];
+    {
+      const int b0 = rs16_base<CH, 8>(cl);
+#pragma unroll
+      for (int j = 0; j < CF; ++j) {
+        const int row = 4 * (P0 + b0 + j) + g;  // < KP: in the k-vector
+        a1[j] = add1 >= 0 ? LDS(add1 + row) : 0.0;
+        a2[j] = LDS(add2 + row);
+      }
+    }
     double P[CH];
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
@@ -2054,14 +2275,13 @@ struct Small {
     }
     int base = 0;
     rs16<CH, 8>(P, cl, base);
-    constexpr int CF = RSCount<CH, 8>::value;
 #pragma unroll
     for (int j = 0; j < CF; ++j) {
       const int row = 4 * (P0 + base + j) + g;
       if (row < k) {
         double v = P[j];
-        if (add1 >= 0) v = v + LDS(add1 + row);
-        v = v - LDS(add2 + row);
+        if (add1 >= 0) v = v + a1[j];
+        v = v - a2[j];
         LDS(out + row) = v;
       }
     }
@@ -2126,17 +2346,33 @@ struct Small {
     }
   }
 
-  // acc[q] (all lanes) = (G' v)[16q+cl]
+  // acc[q] (all lanes) = (G' v)[16q+cl].  The v reads of the next batch of
+  // row steps are issued before the current batch's products (one exposed
+  // LDS round trip per call, not one per pair of row steps).
   __device__ __forceinline__ void gemv_Gt(int v, double (&acc)[NQ]) {
     MARK_BEGIN("gemv_Gt");
     LANE_IDS();
+    constexpr int VB = 8;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+    double vb[VB];
 #pragma unroll
-    for (int pp = 0; pp < NP; ++pp) {
-      const double vp = LDS(v + 4 * pp + g);
+    for (int j = 0; j < VB; ++j) vb[j] = j < NP ? LDS(v + 4 * j + g) : 0.0;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc[q] = fma(a_get(G[pp][q]), vp, acc[q]);
+    for (int p0 = 0; p0 < NP; p0 += VB) {
+      double vn[VB];
+#pragma unroll
+      for (int j = 0; j < VB; ++j) vn[j] = p0 + VB + j < NP ? LDS(v + 4 * (p0 + VB + j) + g) : 0.0;
+      SCHED_FENCE();
+#pragma unroll
+      for (int j = 0; j < VB; ++j) {
+        if (p0 + j < NP) {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) acc[q] = fma(a_get(G[p0 + j < NP ? p0 + j : 0][q]), vb[j], acc[q]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < VB; ++j) vb[j] = vn[j];
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -2152,7 +2388,8 @@ struct Small {
                                  ? (SOCP_LDS_BATCH / NQ > 0 ? SOCP_LDS_BATCH / NQ : 1)
                                  : 1;
   // acc[q] (all lanes) = (A' v)[16q+cl]: rows split over the 4 lane groups
-  __device__ __forceinline__ void At_mv(int v, double (&acc)[NQ], int base = O_A) {
+  // vr (optional): v in registers, vr[s] = v[g + 4s] (s < 4 MQ), instead of LDS
+  __device__ __forceinline__ void At_mv(int v, double (&acc)[NQ], int base = O_A, const double* vr = nullptr) {
     MARK_BEGIN("At_mv");
     LANE_IDS();
 #pragma unroll
@@ -2166,7 +2403,7 @@ struct Small {
 #pragma unroll
       for (int s = 0; s < ATB; ++s) {
         const int i = g + 4 * (s0 + s);
-        vi[s] = LDS(v + i);
+        vi[s] = vr ? vr[s0 + s] : LDS(v + i);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) av[s][q] = LDS(base + i * LDA + 16 * q + cl);
       }
@@ -2215,13 +2452,16 @@ struct Small {
 
   // A_mv with u in row layout in registers (tv[P][r] = u[16P+g+4r], trsv_fwd_r's
   // output): the same products in the same order
-  __device__ __forceinline__ double A_mv_r(const double (&tv)[NQ][4], int sub, int out, int base) {
+  // (mc: the result in column layout in every lane, mc[tm] = out[16 tm + cl],
+  // 0 for rows >= m)
+  __device__ __forceinline__ double A_mv_r(const double (&tv)[NQ][4], int sub, int out, int base, double (&mc)[MQ]) {
     MARK_BEGIN("A_mv");
     LANE_IDS();
     double sq = 0.0;
 #pragma unroll
     for (int tm = 0; tm < MQ; ++tm) {
       const int i = 16 * tm + cl;
+      const double sb = LDS(sub + i);
       double acc = 0.0;
 #pragma unroll
       for (int t0 = 0; t0 < NQ * 4; t0 += AMB) {
@@ -2233,11 +2473,12 @@ struct Small {
         for (int t = 0; t < AMB; ++t) acc = fma(av[t], tv[(t0 + t) >> 2][(t0 + t) & 3], acc);
       }
       acc = rows_sum(acc);
+      const double v = acc - sb;
       if (g == 0 && i < m) {
-        const double v = acc - LDS(sub + i);
         LDS(out + i) = v;
         sq = fma(v, v, sq);
       }
+      mc[tm] = i < m ? v : 0.0;
     }
     return sq;
   }
@@ -2247,6 +2488,20 @@ struct Small {
     MARK_BEGIN("residuals");
     LANE_IDS();
     double acc[NQ], at[NQ];
+    // the small operands read up front, in one round trip: c and x (column
+    // layout), z and s (slot layout)
+    constexpr int NS = KP > 64 ? 2 : 1;
+    double cq[NQ], xq[NQ], zv[NS], sv[NS];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      cq[q] = LDS(C_ + 16 * q + cl);
+      xq[q] = LDS(X_ + 16 * q + cl);
+    }
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      zv[t] = LDS(Z_ + 64 * t + lane);
+      sv[t] = LDS(S_ + 64 * t + lane);
+    }
 #ifndef SOCP_RESID_MERGE
 #define SOCP_RESID_MERGE 0
 #endif
@@ -2280,7 +2535,7 @@ struct Small {
       for (int q = 0; q < NQ; ++q) {
         const int j = 16 * q + cl;
         if (j < n) {
-          const double v = (at[q] + acc[q]) + LDS(C_ + j);
+          const double v = (at[q] + acc[q]) + cq[q];
           LDS(RD + j) = v;
           d2 = fma(v, v, d2);
         }
@@ -2290,9 +2545,11 @@ struct Small {
 #if SOCP_RESID_MERGE
     SYNC();
 #else
-    if (!(SOCP_KO & 16)) gemv_G(X_, S_, H_, DZ);
+    if (!(SOCP_KO & 16)) gemv_G_r(xq, S_, H_, DZ);
 #endif
-    for (int i = lane; i < k; i += 64) zs += LDS(Z_ + i) * LDS(S_ + i);
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+      if (64 * t + lane < k) zs += zv[t] * sv[t];
     if (SOCP_KO & 64) {
       nd = np_ = gap = d2 + p2 + zs;
     } else {
@@ -2351,23 +2608,43 @@ struct Small {
     } else
       symv<NQ>(T, N0, TN);   // Li n0
     STAMP_X(5);
+    // CHOL with one S tile: m0, cy and the next m0 stay in registers
+    constexpr bool MREG = CHOL && MQ == 1;
+    double m0c[MQ], m0r[4];
     if (SOCP_KO & 2048) {
       for (int j = lane; j < m; j += 64) LDS(M0 + j) = LDS(TN + j);
     } else if constexpr (CHOL)
-      A_mv_r(tv, RP, M0, O_AL);  // m0 = A Li n0 - dy = Z't - dy
+      A_mv_r(tv, RP, M0, O_AL, m0c);  // m0 = A Li n0 - dy = Z't - dy
     else if constexpr (AL_LDS)
       A_mv(N0, RP, M0, O_AL);  // m0 = (A Li) n0 - dy: no wait for Li n0
     else
       A_mv(TN, RP, M0);        // m0 = A (Li n0) - dy
-    SYNC();
-    if (SOCP_KO & 2048) {
-      for (int j = lane; j < m; j += 64) LDS(RY + j) = LDS(M0 + j);
-      SYNC();
+    if constexpr (MREG) {
+      if (SOCP_KO & 2048) {
+        SYNC();
+        for (int j = lane; j < m; j += 64) LDS(RY + j) = LDS(M0 + j);
+        SYNC();
+        for (int s = 0; s < 4; ++s) m0r[s] = LDS(RY + g + 4 * s);
+      } else {
+        double rp[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) rp[s] = LDS(RP + g + 4 * s);
+        symv1_r(Sv[0], m0c[0], RY, m0r);  // cy = S^-1 m0
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          m0r[s] = g + 4 * s < m ? ((sing && !init) ? rp[s] - m0r[s] : -m0r[s]) : 0.0;
+      }
     } else {
-      symv<MQ>(Sv, M0, RY);  // cy = S^-1 m0
+      SYNC();
+      if (SOCP_KO & 2048) {
+        for (int j = lane; j < m; j += 64) LDS(RY + j) = LDS(M0 + j);
+        SYNC();
+      } else {
+        symv<MQ>(Sv, M0, RY);  // cy = S^-1 m0
+      }
+      if (lane < m) LDS(M0 + lane) = (sing && !init) ? LDS(RP + lane) - LDS(RY + lane) : -LDS(RY + lane);
+      SYNC();
     }
-    if (lane < m) LDS(M0 + lane) = (sing && !init) ? LDS(RP + lane) - LDS(RY + lane) : -LDS(RY + lane);
-    SYNC();
     STAMP_X(6);
     if constexpr (KEEP_AL) {
       // cx = Li (n0 + A'm0) = Li n0 + (A Li)' m0
@@ -2375,15 +2652,17 @@ struct Small {
     } else if constexpr (AL_LDS) {
       // cx = Li (n0 + A'm0) = Li n0 + (A Li)' m0: one Li product per solve
       // (CHOL: cx = L^-T (t + Z m0))
-      double at[NQ];
+      double at[NQ], tn[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) tn[q] = LDS(TN + 16 * q + cl);  // read with At_mv's operands
       if (SOCP_KO & 2048) {
         for (int q = 0; q < NQ; ++q) at[q] = 0.0;
       } else {
-        At_mv(M0, at, O_AL);
+        At_mv(M0, at, O_AL, MREG ? m0r : nullptr);
       }
       if (g == 0) {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) LDS(RX + 16 * q + cl) = LDS(TN + 16 * q + cl) + at[q];
+        for (int q = 0; q < NQ; ++q) LDS(RX + 16 * q + cl) = tn[q] + at[q];
       }
       SYNC();
       if constexpr (CHOL) {
