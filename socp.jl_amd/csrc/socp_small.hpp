@@ -221,6 +221,37 @@ __device__ __forceinline__ double a_get(const AD& r) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// A row step of G (NQ doubles) out of its AGPRs in ONE asm statement: the
+// compiler pads one wait state after an asm that defines a VGPR a VALU op
+// reads next, so reading the row together pays it once per row, not per value.
+template <int NQ>
+__device__ __forceinline__ void a_get_row(const AD (&r)[NQ], double (&out)[NQ]) {
+  uint32_t lo[4], hi[4];
+  if constexpr (NQ == 1) {
+    asm("v_accvgpr_read_b32 %0, %2\n\tv_accvgpr_read_b32 %1, %3" : "=v"(lo[0]), "=v"(hi[0]) : "a"(r[0].lo), "a"(r[0].hi));
+  } else if constexpr (NQ == 2) {
+    asm("v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\tv_accvgpr_read_b32 %2, %6\n\t"
+        "v_accvgpr_read_b32 %3, %7"
+        : "=v"(lo[0]), "=v"(hi[0]), "=v"(lo[1]), "=v"(hi[1])
+        : "a"(r[0].lo), "a"(r[0].hi), "a"(r[1].lo), "a"(r[1].hi));
+  } else if constexpr (NQ == 3) {
+    asm("v_accvgpr_read_b32 %0, %6\n\tv_accvgpr_read_b32 %1, %7\n\tv_accvgpr_read_b32 %2, %8\n\t"
+        "v_accvgpr_read_b32 %3, %9\n\tv_accvgpr_read_b32 %4, %10\n\tv_accvgpr_read_b32 %5, %11"
+        : "=v"(lo[0]), "=v"(hi[0]), "=v"(lo[1]), "=v"(hi[1]), "=v"(lo[2]), "=v"(hi[2])
+        : "a"(r[0].lo), "a"(r[0].hi), "a"(r[1].lo), "a"(r[1].hi), "a"(r[2].lo), "a"(r[2].hi));
+  } else {
+    static_assert(NQ == 4, "NQ <= 4");
+    asm("v_accvgpr_read_b32 %0, %8\n\tv_accvgpr_read_b32 %1, %9\n\tv_accvgpr_read_b32 %2, %10\n\t"
+        "v_accvgpr_read_b32 %3, %11\n\tv_accvgpr_read_b32 %4, %12\n\tv_accvgpr_read_b32 %5, %13\n\t"
+        "v_accvgpr_read_b32 %6, %14\n\tv_accvgpr_read_b32 %7, %15"
+        : "=v"(lo[0]), "=v"(hi[0]), "=v"(lo[1]), "=v"(hi[1]), "=v"(lo[2]), "=v"(hi[2]), "=v"(lo[3]), "=v"(hi[3])
+        : "a"(r[0].lo), "a"(r[0].hi), "a"(r[1].lo), "a"(r[1].hi), "a"(r[2].lo), "a"(r[2].hi), "a"(r[3].lo),
+          "a"(r[3].hi));
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) out[q] = __longlong_as_double((long long)(((uint64_t)hi[q] << 32) | lo[q]));
+}
+
 // a_get for a value consumed directly as an MFMA A/B operand: v_accvgpr_read is
 // a VALU write, and VALU write -> MFMA operand read needs 2 wait states, which
 // hipcc does not insert for a producer inside inline asm (it pads one state).
@@ -306,6 +337,43 @@ __device__ __forceinline__ double rows_sum(double x) {
 // gets the total, no predicates, no LDS.  MX: max instead of sum.
 template <bool MX>
 __device__ __forceinline__ double rop(double a, double b) { return MX ? fmax(a, b) : a + b; }
+// Several independent values at once, step by step (each DPP step of one
+// chain waits on its predecessor; interleaving the chains fills those wait
+// states).  The same operations in the same order per value as
+// cone_allreduce_rows.  MXM: bit q set = max for value q.
+template <int NV, unsigned MXM>
+__device__ __forceinline__ void cone_allreduce_rows_n(double (&v)[NV], int R) {
+#define SOCP_AR_STEP(CTRL)                                                                          \
+  _Pragma("unroll") for (int q = 0; q < NV; ++q) {                                                  \
+    const double y = dpp_all<CTRL>(v[q]);                                                           \
+    v[q] = ((MXM >> q) & 1) ? fmax(v[q], y) : v[q] + y;                                             \
+  }
+  SOCP_AR_STEP(0x128)
+  SOCP_AR_STEP(0x124)
+  SOCP_AR_STEP(0x122)
+  SOCP_AR_STEP(0x121)
+#undef SOCP_AR_STEP
+  if (R >= 2) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const unsigned lo = (unsigned)__double2loint(v[q]), hi = (unsigned)__double2hiint(v[q]);
+      const auto c = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+      const auto d = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+      const double a = __hiloint2double((int)d[0], (int)c[0]), b = __hiloint2double((int)d[1], (int)c[1]);
+      v[q] = ((MXM >> q) & 1) ? fmax(a, b) : a + b;
+    }
+  }
+  if (R == 4) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const unsigned lo = (unsigned)__double2loint(v[q]), hi = (unsigned)__double2hiint(v[q]);
+      const auto c = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+      const auto d = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+      const double a = __hiloint2double((int)d[0], (int)c[0]), b = __hiloint2double((int)d[1], (int)c[1]);
+      v[q] = ((MXM >> q) & 1) ? fmax(a, b) : a + b;
+    }
+  }
+}
 template <bool MX>
 __device__ __forceinline__ double cone_allreduce_rows(double v, int R) {
   v = rop<MX>(v, dpp_all<0x128>(v));  // row_ror:8
@@ -768,12 +836,24 @@ struct Small {
     ko_gloaded = true;
     // G -> AGPRs.  a_put is an asm statement the scheduler does not move loads
     // across, so the loads are issued in batches of 16 into VGPRs first (one
-    // HBM round trip per batch, not per element).  Padding (row >= k or
-    // col >= n) reads element 0 and is zeroed with an integer mask.
+    // HBM round trip per batch, not per element).  Raw buffer loads over the
+    // problem's G (k n doubles): a padding element (row >= k or col >= n)
+    // takes an offset past the range and reads 0 -- no address arithmetic in
+    // 64 bits, no branch, no mask per element.
 #ifndef SOCP_GLOAD_BATCH
 #define SOCP_GLOAD_BATCH 16
 #endif
     constexpr int GT = NP * NQ, GB = SOCP_GLOAD_BATCH;
+    // (the base made wave-uniform explicitly: a divergent-looking descriptor
+    // would be waterfall-looped around every load)
+    const uint64_t gpu = (uint64_t)Gp;
+    const uint64_t gbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(gpu >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)gpu);
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)gbase, (short)0, __builtin_amdgcn_readfirstlane(k * n * (int)sizeof(double)), 0x00020000);
+    int colk[NQ];  // byte offset of the lane's column in each column tile, or "out of range"
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) colk[q] = 16 * q + cl < n ? (16 * q + cl) * k * 8 : 0x40000000;
 #pragma unroll
     for (int b0 = 0; b0 < GT; b0 += GB) {
       uint64_t tmp[GB];
@@ -782,10 +862,9 @@ struct Small {
         const int e = b0 + t;
         if (e < GT) {
           const int pp = e / NQ, q = e % NQ;
-          const int row = 4 * pp + g, col = 16 * q + cl;
-          const int ok = (row < k) & (col < n);
-          const int64_t idx = ok ? (int64_t)col * k + row : 0;
-          tmp[t] = (uint64_t)__double_as_longlong(Gp[idx]) & (0ull - (uint64_t)ok);
+          const int row = 4 * pp + g;
+          const int off = row < k ? colk[q] + row * 8 : 0x40000000;
+          tmp[t] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(grs, off, 0, 0));
         }
       }
 #pragma unroll
@@ -888,11 +967,17 @@ struct Small {
     constexpr int NS = KP > 64 ? 2 : 1;  // slots that can hold elements of this shape
     if (a.al_rows) {  // row-aligned cones: registers only
       const int R = a.al_rows;
+      constexpr unsigned MXM = NS == 2 ? (MX | (MX << NV)) : MX;
+      double w[NS * NV];
 #pragma unroll
       for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int q = 0; q < NV; ++q)
-          v[s][q] = ((MX >> q) & 1) ? cone_allreduce_rows<true>(v[s][q], R) : cone_allreduce_rows<false>(v[s][q], R);
+        for (int q = 0; q < NV; ++q) w[s * NV + q] = v[s][q];
+      cone_allreduce_rows_n<NS * NV, MXM>(w, R);
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int q = 0; q < NV; ++q) v[s][q] = w[s * NV + q];
       return;
     }
     const int rl = lane & 15;
@@ -951,10 +1036,16 @@ struct Small {
     const int rl = lane & 15;
     if (a.al_rows) {  // row-aligned cones: every lane of the cone gets its total
       const int R = a.al_rows;
+      double w[NS * NV];
 #pragma unroll
       for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int q = 0; q < NV; ++q) v[s][q] = cone_allreduce_rows<false>(v[s][q], R);
+        for (int q = 0; q < NV; ++q) w[s * NV + q] = v[s][q];
+      cone_allreduce_rows_n<NS * NV, 0u>(w, R);
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int q = 0; q < NV; ++q) v[s][q] = w[s * NV + q];
     } else {
 #define SOCP_SCAN_STEP(CTRL, OK)                         \
   _Pragma("unroll") for (int s = 0; s < NS; ++s) {       \
@@ -1482,8 +1573,12 @@ struct Small {
           const bool in = row >= o && row < o + d;
           const double wu = in ? (row == o ? hw : w[u]) : 0.0;
           if (pb + u < NP) {
+            {
+              double gr[NQ];
+              a_get_row<NQ>(G[pb + u < NP ? pb + u : 0], gr);
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) acc[q] = fma(wu, a_get(G[pb + u < NP ? pb + u : 0][q]), acc[q]);
+              for (int q = 0; q < NQ; ++q) acc[q] = fma(wu, gr[q], acc[q]);
+            }
           }
         }
       }
@@ -1534,8 +1629,12 @@ struct Small {
     double u[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) u[q] = LDS(c.ub + 16 * q);
+    {
+      double gr[NQ];
+      a_get_row<NQ>(G[pp], gr);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) X[q] = fma(c.ca, a_get(G[pp][q]), c.cb * u[q]);
+      for (int q = 0; q < NQ; ++q) X[q] = fma(c.ca, gr[q], c.cb * u[q]);
+    }
   }
   __device__ __forceinline__ void form_H(bool addAA) {
     MARK_BEGIN("form_H");
@@ -2269,8 +2368,12 @@ struct Small {
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
       double acc = 0.0;
+      {
+        double gr[NQ];
+        a_get_row<NQ>(G[P0 + j], gr);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc = fma(a_get(G[P0 + j][q]), uq[q], acc);
+        for (int q = 0; q < NQ; ++q) acc = fma(gr[q], uq[q], acc);
+      }
       P[j] = acc;
     }
     int base = 0;
@@ -2367,8 +2470,12 @@ struct Small {
 #pragma unroll
       for (int j = 0; j < VB; ++j) {
         if (p0 + j < NP) {
+          {
+            double gr[NQ];
+            a_get_row<NQ>(G[p0 + j < NP ? p0 + j : 0], gr);
 #pragma unroll
-          for (int q = 0; q < NQ; ++q) acc[q] = fma(a_get(G[p0 + j < NP ? p0 + j : 0][q]), vb[j], acc[q]);
+            for (int q = 0; q < NQ; ++q) acc[q] = fma(gr[q], vb[j], acc[q]);
+          }
         }
       }
 #pragma unroll
