@@ -2155,6 +2155,7 @@ struct Large {
     int it = 0;
     while (go) {
       LSTAMP(SP_OTHER);
+      if (it >= a.maxit && !a.res) break;  // no residuals after the last iteration (solver.jl:105-151)
       residuals(nd, np_, gap);
       LSTAMP(SP_RESID);
       if (it >= a.maxit) break;

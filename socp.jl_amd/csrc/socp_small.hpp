@@ -3008,6 +3008,13 @@ struct Small {
         case MP_ITER: {  // residuals (solver.jl:109-118), compute_scaling (:106), exit test (:122)
           MARK_BEGIN("case MP_ITER");
           STAMP(SP_OTHER);
+          // after the last iteration the reference loop ends without another
+          // residual evaluation (solver.jl:105-151): they are formed then only
+          // when the caller asked for the final residual norms
+          if (it >= a.maxit && !a.res) {
+            done = true;
+            break;
+          }
           if (SOCP_KO & 2) {
             nd = np_ = gap = 1.0;
           } else {
