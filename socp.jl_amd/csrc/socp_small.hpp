@@ -832,6 +832,18 @@ struct Small {
     MARK_BEGIN("load_problem");
     LANE_IDS();
     const double* Gp = a.G + p * (int64_t)k * n;
+    // the vectors and the first chunk of A are requested first: their HBM
+    // round trip runs under G's (n, m <= 64 here, k <= 128)
+    const double cv = lane < n ? a.c[p * n + lane] : 0.0;
+    const double bv = lane < m ? a.b[p * m + lane] : 0.0;
+    const double hv0 = lane < k ? a.h[p * k + lane] : 0.0;
+    const double hv1 = lane + 64 < k ? a.h[p * k + 64 + lane] : 0.0;
+    const double* Ap = a.A + p * (int64_t)m * n;
+    const int mn = m * n;
+    constexpr int AB = HOIST_CST ? 16 : 8;
+    double av[AB];
+#pragma unroll
+    for (int t = 0; t < AB; ++t) av[t] = (64 * t + lane < mn) ? Ap[64 * t + lane] : 0.0;
     if (!(SOCP_KO & 1) || !ko_gloaded) {
     ko_gloaded = true;
     // G -> AGPRs.  a_put is an asm statement the scheduler does not move loads
@@ -874,17 +886,6 @@ struct Small {
       }
     }
     }
-    // vectors (n, m <= 64 here, k <= 128), loads first, then the LDS writes
-    const double cv = lane < n ? a.c[p * n + lane] : 0.0;
-    const double bv = lane < m ? a.b[p * m + lane] : 0.0;
-    const double hv0 = lane < k ? a.h[p * k + lane] : 0.0;
-    const double hv1 = lane + 64 < k ? a.h[p * k + 64 + lane] : 0.0;
-    const double* Ap = a.A + p * (int64_t)m * n;
-    const int mn = m * n;
-    constexpr int AB = 8;
-    double av[AB];
-#pragma unroll
-    for (int t = 0; t < AB; ++t) av[t] = (64 * t + lane < mn) ? Ap[64 * t + lane] : 0.0;
     for (int e = lane; e < NKV * SH::KS; e += 64) LDS(O_KV + e) = 0.0;
     for (int e = lane; e < O_U + SH::UAL - O_A; e += 64) LDS(O_A + e) = 0.0;
     SYNC();
