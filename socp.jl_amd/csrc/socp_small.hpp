@@ -2489,12 +2489,11 @@ struct Small {
   }
 
 #ifndef SOCP_LDS_BATCH
-#define SOCP_LDS_BATCH 8  // LDS reads issued per round trip in the A products
+#define SOCP_LDS_BATCH 16  // LDS reads issued per round trip in the A products (8 where HOIST_CST is off)
 #endif
-  static constexpr int AMB = (NQ * 4) % SOCP_LDS_BATCH == 0 ? SOCP_LDS_BATCH : 4;
-  static constexpr int ATB = (MQ * 4) % (SOCP_LDS_BATCH / NQ > 0 ? SOCP_LDS_BATCH / NQ : 1) == 0
-                                 ? (SOCP_LDS_BATCH / NQ > 0 ? SOCP_LDS_BATCH / NQ : 1)
-                                 : 1;
+  static constexpr int LDB = HOIST_CST ? SOCP_LDS_BATCH : 8;
+  static constexpr int AMB = (NQ * 4) % LDB == 0 ? LDB : 4;
+  static constexpr int ATB = (MQ * 4) % (LDB / NQ > 0 ? LDB / NQ : 1) == 0 ? (LDB / NQ > 0 ? LDB / NQ : 1) : 1;
   // acc[q] (all lanes) = (A' v)[16q+cl]: rows split over the 4 lane groups
   // vr (optional): v in registers, vr[s] = v[g + 4s] (s < 4 MQ), instead of LDS
   __device__ __forceinline__ void At_mv(int v, double (&acc)[NQ], int base = O_A, const double* vr = nullptr) {
