@@ -111,9 +111,19 @@ enum : int { KV_H, KV_Z, KV_S, KV_DZ, KV_DS, KV_LAM, KV_WB, KV_CA, KV_CB, KV_IL,
              KV_K1, KV_K2, KV_T1, KV_T2 };
 constexpr int NKV_DEAD = KV_T2 - KV_RZ + 1;
 
+// the A block's leading dimension (Shape::LDA)
+__host__ __device__ constexpr int small_lda(int NQ, int NP) {
+  return (NQ * NP > 24 && NQ > 1) ? 16 * NQ + 2 : 16 * NQ + 1;  // (16 NQ + 2) / 2 is odd
+}
+
 template <int NQ, int NP, int MQ>
 struct Shape {
-  static constexpr int NPAD = 16 * NQ, KP = 4 * NP, MPAD = 16 * MQ, LDA = NPAD + 1;
+  // LDA (row stride of A and of Z' / A Li in LDS): NPAD + 1 on the two-wave
+  // shapes (their LDS is tight); on the others NPAD + 2 = 2 x odd, where the
+  // A x / Z't reads of a half-wave (lanes cl, g in {0, 1}: cl LDA + g doubles)
+  // hit 32 distinct bank pairs, instead of two lanes per pair at NPAD + 1
+  static constexpr int NPAD = 16 * NQ, KP = 4 * NP, MPAD = 16 * MQ,
+                       LDA = small_lda(NQ, NP);
   // k-vector stride KP: lanes read slot 1 / padding elements i >= KP
   // unconditionally and mask the values by their type code (3 = pad), so those
   // reads may alias the next vector (the last one reads into the A block); every
@@ -145,12 +155,12 @@ enum : int { MV_B, MV_Y, MV_RP, MV_RY, MV_M0, MV_TM };
 // tiles in lane order, LAM WB CA CBV IL, the per-cone constants, the sing flag
 inline int64_t small_rec_doubles(int NQ, int NP, int MQ) {
   const int64_t NT = NQ * (NQ + 1) / 2, MT = MQ * (MQ + 1) / 2;
-  const int64_t al = MQ == 1 ? (int64_t)16 * (16 * NQ + 1) : 0;  // A Li kept in LDS (Shape::AL_LDS)
+  const int64_t al = MQ == 1 ? (int64_t)16 * small_lda(NQ, NP) : 0;  // A Li kept in LDS (Shape::AL_LDS)
   return (NT + MT) * 256 + 5 * (int64_t)(4 * NP) + 20 * NCS + al + 8;
 }
 
 inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
-  int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = NPAD + 1;
+  int NPAD = 16 * NQ, MPAD = 16 * MQ, LDA = small_lda(NQ, NP);
   int KS = 4 * NP;  // Shape::KS
   int ual = (MQ == 1 && MPAD * LDA > NCS * NPAD) ? MPAD * LDA : NCS * NPAD;  // Shape::UAL
   const bool tb_alias = MQ == 1 && NKV_DEAD * KS >= 16 * 17;                // Shape::TB_ALIAS
