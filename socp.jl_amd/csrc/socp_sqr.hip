@@ -214,6 +214,12 @@ __device__ __forceinline__ double dot_strided(const double* p, int64_t stride, c
   return acc;
 }
 
+// loads in flight per lane in the solve kernel's passes over G (an HBM round
+// trip per SQR_GU elements; 16: -1.3 % solve kernel time at the C2 shape)
+#ifndef SQR_GU
+#define SQR_GU 16
+#endif
+
 // 1/sqrt(x) from v_rsq_f64 refined by two Newton steps (to within an ulp or
 // two; x <= 0 or NaN gives NaN or inf, which the callers' status checks catch)
 __device__ __forceinline__ double rsqrt_nr(double x) {
@@ -653,7 +659,7 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
   // n0 = G' k1 + dx (+ A' dy)   (:97-102): a lane per column
   double n0 = 0.0;
   if (lane < n) {
-    n0 = dot_strided(G + (int64_t)lane * k, 1, k1, k);
+    n0 = dot_strided<SQR_GU>(G + (int64_t)lane * k, 1, k1, k);
     n0 += a.dx[p * n + lane];
     if (sing) n0 += dot_strided(A + (int64_t)lane * m, 1, a.dy + p * m, m);
   }
@@ -695,7 +701,7 @@ __device__ __forceinline__ void solve_problem(Ctx& C, int64_t p) {
   }
   wsync();
   // k1 = G cx - k2 (:125-126), a lane per row
-  for (int i = lane; i < k; i += 64) kt[i] = dot_strided(G + i, k, nv, n) - k2[i];
+  for (int i = lane; i < k; i += 64) kt[i] = dot_strided<SQR_GU>(G + i, k, nv, n) - k2[i];
   // cz = W^-1 W^-1 k1; k1 = W cz; k0 -= k1; cs = W k0   (:127-131)
   double *cz = k2, *cs = k1;
   for (int c = 0; c < nc; ++c) {
