@@ -1189,7 +1189,7 @@ struct Small {
         LDS(CA + i) = poc ? zi[s] * q : imu;
         LDS(CBV + i) = poc ? 0.0 : wt * imu;
         if (poc) LDS(IL + i) = q;
-        if (write_ds) LDS(DS + i) = poc ? li[s] * li[s] : (l0 * li[s] + l0 * li[s]);
+        if (write_ds) LDS(DS + i) = -(poc ? li[s] * li[s] : (l0 * li[s] + l0 * li[s]));  // -ds: the RHS
       }
       // lam o lam head (vprod!, vectors.jl:58-75) and |lambda_1|^2 (POC: the
       // cone's sum of lambda_i^2, its share of lam'lam), |wbar_1|^2, wbar_1'lambda_1
@@ -1219,7 +1219,7 @@ struct Small {
         LDS(cc(CC_SA, c)) = sa;
         LDS(cc(CC_SAL, c)) = 1.0 / (sa * l0 + 1.0);
         tl = l0 * l0 + l1;
-        if (write_ds) LDS(DS + o) = tl;
+        if (write_ds) LDS(DS + o) = -tl;
       } else {
         tl = l1;
       }
@@ -2360,7 +2360,7 @@ struct Small {
 
   // out[row] = (G u)[row] + add1[row] - add2[row] for rows < k (u in column layout).
   // Rows are reduced over the 16 column lanes in chunks of up to 8 row-steps.
-  template <int P0, int CH>
+  template <int P0, int CH, bool NEG = false>
   __device__ __forceinline__ void gemv_G_chunk(const double (&uq)[NQ], int add1, int add2, int out) {
     LANE_IDS();
     constexpr int CF = RSCount<CH, 8>::value;
@@ -2396,12 +2396,12 @@ struct Small {
         double v = P[j];
         if (add1 >= 0) v = v + a1[j];
         v = v - a2[j];
-        LDS(out + row) = v;
+        LDS(out + row) = NEG ? -v : v;
       }
     }
     if constexpr (P0 + CH < NP) {
       constexpr int NXT = (NP - P0 - CH) < 8 ? (NP - P0 - CH) : 8;
-      gemv_G_chunk<P0 + CH, NXT>(uq, add1, add2, out);
+      gemv_G_chunk<P0 + CH, NXT, NEG>(uq, add1, add2, out);
     }
   }
   __device__ __forceinline__ void gemv_G(int u, int add1, int add2, int out) {
@@ -2413,10 +2413,12 @@ struct Small {
     gemv_G_chunk<0, (NP < 8 ? NP : 8)>(uq, add1, add2, out);
     SYNC();
   }
-  // the same with u in column layout in registers (uq[q] = u[16q+cl])
+  // the same with u in column layout in registers (uq[q] = u[16q+cl]); NEG:
+  // store the negated rows
+  template <bool NEG = false>
   __device__ __forceinline__ void gemv_G_r(const double (&uq)[NQ], int add1, int add2, int out) {
     MARK_BEGIN("gemv_G");
-    gemv_G_chunk<0, (NP < 8 ? NP : 8)>(uq, add1, add2, out);
+    gemv_G_chunk<0, (NP < 8 ? NP : 8), NEG>(uq, add1, add2, out);
     SYNC();
   }
 
@@ -2537,7 +2539,7 @@ struct Small {
   }
   // out[i] = (A u)[i] - sub[i] for i < m (columns split over the 4 lane groups);
   // returns sum of out[i]^2 on lanes g == 0
-  __device__ __forceinline__ double A_mv(int u, int sub, int out, int base = O_A) {
+  __device__ __forceinline__ double A_mv(int u, int sub, int out, int base = O_A, bool neg = false) {
     MARK_BEGIN("A_mv");
     LANE_IDS();
     double sq = 0.0;
@@ -2560,7 +2562,7 @@ struct Small {
       acc = rows_sum(acc);
       if (g == 0 && i < m) {
         const double v = acc - LDS(sub + i);
-        LDS(out + i) = v;
+        LDS(out + i) = neg ? -v : v;
         sq = fma(v, v, sq);
       }
     }
@@ -2653,16 +2655,16 @@ struct Small {
         const int j = 16 * q + cl;
         if (j < n) {
           const double v = (at[q] + acc[q]) + cq[q];
-          LDS(RD + j) = v;
+          LDS(RD + j) = -v;  // the residuals are stored negated: the affine RHS (solver.jl:124)
           d2 = fma(v, v, d2);
         }
       }
     }
-    const double p2 = (SOCP_KO & 128) ? 0.0 : A_mv(X_, B_, RP);
+    const double p2 = (SOCP_KO & 128) ? 0.0 : A_mv(X_, B_, RP, O_A, true);
 #if SOCP_RESID_MERGE
     SYNC();
 #else
-    if (!(SOCP_KO & 16)) gemv_G_r(xq, S_, H_, DZ);
+    if (!(SOCP_KO & 16)) gemv_G_r<true>(xq, S_, H_, DZ);
 #endif
 #pragma unroll
     for (int t = 0; t < NS; ++t)
@@ -3047,13 +3049,7 @@ struct Small {
             done = true;
             break;
           }
-          for (int j = lane; j < n; j += 64) LDS(RD + j) = -LDS(RD + j);
-          for (int i = lane; i < m; i += 64) LDS(RP + i) = -LDS(RP + i);
-          for (int i = lane; i < k; i += 64) {
-            LDS(DZ + i) = -LDS(DZ + i);
-            LDS(DS + i) = -LDS(DS + i);
-          }
-          SYNC();
+          // (rmul!(dx, -1) etc., solver.jl:124: the residuals and ds were stored negated)
           fac_ident = false;
           fac_aa = sing;
           fret = MP_SOLVE_HEAD;
@@ -3131,11 +3127,29 @@ struct Small {
             }
             // combined direction: step and update (solver.jl:143-150)
             const double stp = tstep * a.step;
-            for (int j = lane; j < n; j += 64) LDS(X_ + j) = LDS(X_ + j) + LDS(RX + j) * stp;
-            for (int i = lane; i < m; i += 64) LDS(Y_ + i) = LDS(Y_ + i) + LDS(RY + i) * stp;
-            for (int i = lane; i < k; i += 64) {
-              LDS(Z_ + i) = LDS(Z_ + i) + LDS(RZ + i) * stp;
-              LDS(S_ + i) = LDS(S_ + i) + LDS(RS + i) * stp;
+            {  // every read first (n, m <= 64, k <= 128 here), then the updates
+              constexpr int NS = KP > 64 ? 2 : 1;
+              const int ly = lane < MPAD ? lane : 0;
+              const double xo = LDS(X_ + lane), rx = LDS(RX + lane), yo = LDS(Y_ + ly), ry = LDS(RY + ly);
+              double zo[NS], rz[NS], so[NS], rs[NS];
+#pragma unroll
+              for (int t = 0; t < NS; ++t) {
+                const int i = 64 * t + lane;
+                zo[t] = LDS(Z_ + i);
+                rz[t] = LDS(RZ + i);
+                so[t] = LDS(S_ + i);
+                rs[t] = LDS(RS + i);
+              }
+              if (lane < n) LDS(X_ + lane) = xo + rx * stp;
+              if (lane < m) LDS(Y_ + lane) = yo + ry * stp;
+#pragma unroll
+              for (int t = 0; t < NS; ++t) {
+                const int i = 64 * t + lane;
+                if (i < k) {
+                  LDS(Z_ + i) = zo[t] + rz[t] * stp;
+                  LDS(S_ + i) = so[t] + rs[t] * stp;
+                }
+              }
             }
             SYNC();
             STAMP(SP_STEP);
