@@ -572,6 +572,11 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
   e = fma(-(h * y), y, 0.5);
   return fma(y, e, y);
 }
+// square root through rsqrt_nr (0 and +inf passed through, negative -> NaN)
+__device__ __forceinline__ double sqrt_nr(double d) {
+  const double r = d * rsqrt_nr(d);
+  return (d == 0.0 || d == INFINITY) ? d : r;
+}
 // the tile factorisation's pivots: SOCP_TILE_NEWTON Newton steps (1: a
 // shorter dependency chain, within a few ulp)
 #ifndef SOCP_TILE_NEWTON
@@ -1137,24 +1142,25 @@ struct Small {
       const int c = lane, o = HOIST_CST ? lc_off : (int)LDS(O_COFF + c);
       const double z0 = LDS(Z_ + o), s0 = LDS(S_ + o);
       const double onrmz = z0 * z0 - cone_tot(0, c), onrms = s0 * s0 - cone_tot(1, c);
-      const double nrmz = sqrt(onrmz), nrms = sqrt(onrms);
-      const double fz = 1.0 / nrmz, fs = 1.0 / nrms;
+      // the square roots and their reciprocals from one Newton-refined rsq each
+      const double fz = rsqrt_nr(onrmz), fs = rsqrt_nr(onrms);
+      const double nrmz = onrmz * fz, nrms = onrms * fs;
       const double zb0 = z0 * fz, sb0 = s0 * fs;
       const double nsum = zb0 * sb0 + cone_tot(2, c) * fz * fs;
-      const double garg = (1.0 + nsum) / 2.0;
-      const double gamma = sqrt(garg);
-      const double fg = 1.0 / (2.0 * gamma);
+      const double garg = (1.0 + nsum) * 0.5;
+      const double rg = rsqrt_nr(garg);
+      const double gamma = garg * rg;
+      const double fg = 0.5 * rg;
       const double wb0 = (sb0 + zb0) * fg;
-      const double ratio = nrms / nrmz, prod = nrms * nrmz;
-      const double mu = sqrt(ratio), tmv1 = sqrt(prod);
-      const double mult = tmv1 / (zb0 + sb0 + 2.0 * gamma);
+      const double ratio = nrms * fz, prod = nrms * nrmz;
+      const double im = rsqrt_nr(ratio), mu = ratio * im, tmv1 = sqrt_nr(prod);
+      const double mult = tmv1 * recip(zb0 + sb0 + 2.0 * gamma);
       const double l0 = gamma * tmv1;
-      const double im = 1.0 / mu;
       dm = (onrmz < 0.0) || (onrms < 0.0) || (garg < 0.0) || (ratio < 0.0) || (prod < 0.0);
       LDS(cc(CC_MU, c)) = mu;
       LDS(cc(CC_IMU, c)) = im;
       LDS(cc(CC_WB0, c)) = wb0;
-      LDS(cc(CC_I1, c)) = 1.0 / (1.0 + wb0);
+      LDS(cc(CC_I1, c)) = recip(1.0 + wb0);
       LDS(cc(CC_L0, c)) = l0;
       LDS(cc(CC_AS, c)) = fs * fg;  // wbar_i = (s_i/|s| - z_i/|z|) / (2 gamma)
       LDS(cc(CC_AZ, c)) = fz * fg;
@@ -1209,15 +1215,15 @@ struct Small {
         const double l0 = LDS(cc(CC_L0, c));
         const double aa = l0 * l0 - l1;
         da = aa < 0.0;
-        const double sa = 1.0 / sqrt(aa);
+        const double sa = rsqrt_nr(aa);
         LDS(cc(CC_W2, c)) = cone_tot(1, c);
         LDS(cc(CC_WL, c)) = cone_tot(2, c);
         LDS(cc(CC_AA, c)) = aa;
-        LDS(cc(CC_IAA, c)) = 1.0 / aa;
-        LDS(cc(CC_IL0, c)) = 1.0 / l0;
-        LDS(cc(CC_IL0AA, c)) = 1.0 / (l0 * aa);
+        LDS(cc(CC_IAA, c)) = recip(aa);
+        LDS(cc(CC_IL0, c)) = recip(l0);
+        LDS(cc(CC_IL0AA, c)) = recip(l0 * aa);
         LDS(cc(CC_SA, c)) = sa;
-        LDS(cc(CC_SAL, c)) = 1.0 / (sa * l0 + 1.0);
+        LDS(cc(CC_SAL, c)) = recip(sa * l0 + 1.0);
         tl = l0 * l0 + l1;
         if (write_ds) LDS(DS + o) = -tl;
       } else {
@@ -1439,15 +1445,15 @@ struct Small {
       if (64 * s >= k || kd[s] == 3 || 64 * s + lane != eo[s]) continue;
       const double sa = CST(8, ccv(CC_SA, c));
 #undef CST
-      const double vy = sqrt(w[s][0]) - sa * r1y[s];
-      const double vk = sqrt(w[s][1]) - sa * r1k[s];
+      const double vy = sqrt_nr(w[s][0]) - sa * r1y[s];
+      const double vk = sqrt_nr(w[s][1]) - sa * r1k[s];
       LDS(O_TOTC + c) = kd[s] == 0 ? fmax(w[s][2], w[s][3]) : fmax(vy, vk);
       LDS(cc(CC_KK, c)) = w[s][4];
     }
     SYNC();
     dom = dm_aa ? 1 : 0;
     const double t = fmax(cone_max(0), 0.0);
-    return (t == 0.0) ? 1.0 : fmin(1.0, 1.0 / t);
+    return !(t > 1.0) ? 1.0 : (t == INFINITY ? 0.0 : recip(t));  // min(1, 1/t)
   }
 
   // rho, sigma, mu (solver.jl:132-134) and the corrector right-hand side
@@ -1532,7 +1538,7 @@ struct Small {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if (64 * s >= k || kd[s] == 3 || 64 * s + lane != eo[s]) continue;
-      const double nr = sqrt(v[s][0]);
+      const double nr = sqrt_nr(v[s][0]);
       const bool poc = kd[s] == 0;
       LDS(O_TOTC + ci[s]) = poc ? v[s][1] : nr + x0[s];
       LDS(O_TOTC + NCS + ci[s]) = poc ? v[s][2] : nr - x0[s];
