@@ -72,7 +72,7 @@ __device__ __forceinline__ void cone_scale(const double* wb, double mu, const do
                            int kind, bool inv, int lane) {
   wsync();
   if (kind == POC_K) {
-    for (int i = o + lane; i < o + d; i += 64) op[i] = inv ? 1.0 / wb[i] * x[i] : wb[i] * x[i];
+    for (int i = o + lane; i < o + d; i += 64) op[i] = inv ? recip(wb[i]) * x[i] : wb[i] * x[i];
     return;
   }
   double part = 0.0;
@@ -80,12 +80,12 @@ __device__ __forceinline__ void cone_scale(const double* wb, double mu, const do
   const double del = wave_sum(part);
   const double x0 = x[o], w0 = wb[o];
   if (inv) {
-    const double cst = (-x0 + del / (1.0 + w0));
-    const double im = 1.0 / mu;
+    const double cst = (-x0 + del * recip(1.0 + w0));
+    const double im = recip(mu);
     for (int i = o + 1 + lane; i < o + d; i += 64) op[i] = im * (x[i] + cst * wb[i]);
     if (lane == 0) op[o] = im * (w0 * x0 - del);
   } else {
-    const double cst = (x0 + del / (1.0 + w0));
+    const double cst = (x0 + del * recip(1.0 + w0));
     for (int i = o + 1 + lane; i < o + d; i += 64) op[i] = mu * (x[i] + cst * wb[i]);
     if (lane == 0) op[o] = mu * (w0 * x0 + del);
   }
@@ -96,7 +96,7 @@ __device__ __forceinline__ void cone_scale(const double* wb, double mu, const do
 __device__ __forceinline__ void cone_iprod(const double* lam, const double* v, double* t, int o, int d, int kind, int lane) {
   wsync();
   if (kind == POC_K) {
-    for (int i = o + lane; i < o + d; i += 64) t[i] = v[i] / lam[i];
+    for (int i = o + lane; i < o + d; i += 64) t[i] = v[i] * recip(lam[i]);
     return;
   }
   double p1 = 0.0, p2 = 0.0;
@@ -107,9 +107,10 @@ __device__ __forceinline__ void cone_iprod(const double* lam, const double* v, d
   const double ll = wave_sum(p1), lv = wave_sum(p2);
   const double l0 = lam[o], v0 = v[o];
   const double a = l0 * l0 - ll;
+  const double ia = recip(a), il0 = recip(l0), ila = recip(l0 * a);
   for (int i = o + 1 + lane; i < o + d; i += 64)
-    t[i] = -v0 * lam[i] / a + v[i] / l0 + lam[i] * lv / (l0 * a);
-  if (lane == 0) t[o] = v0 * l0 / a - lv / a;
+    t[i] = -v0 * lam[i] * ia + v[i] * il0 + lam[i] * lv * ila;
+  if (lane == 0) t[o] = v0 * l0 * ia - lv * ia;
   wsync();
 }
 
@@ -125,12 +126,13 @@ __device__ __forceinline__ void sqr_scaling_cone(Ctx& C, int c) {
   bool bad = false;
   if (kind == POC_K) {
     for (int i = o + C.lane; i < o + d; i += 64) {
-      const double zs = z[i] / s[i], sz = s[i] * z[i], sdz = s[i] / z[i];
-      bad |= zs < 0.0 || sz < 0.0 || sdz < 0.0;
-      D[i] = zs;
-      iW[i] = sqrt(zs);
-      lam[i] = sqrt(sz);
-      wb[i] = sqrt(sdz);
+      // one rsq of s z gives sqrt(z/s) = z q, sqrt(s z) = (s z) q, sqrt(s/z) = s q
+      const double sz = s[i] * z[i], q = rsqrt_nr(sz);
+      bad |= sz < 0.0;
+      D[i] = z[i] * recip(s[i]);
+      iW[i] = z[i] * q;
+      lam[i] = sz * q;
+      wb[i] = s[i] * q;
       u[i] = 0.0;
       v[i] = 0.0;
     }
@@ -143,41 +145,42 @@ __device__ __forceinline__ void sqr_scaling_cone(Ctx& C, int c) {
     }
     const double sprod = s[o] * s[o] - wave_sum(ps), zprod = z[o] * z[o] - wave_sum(pz);
     bad |= sprod < 0.0 || zprod < 0.0;
-    const double fs = 1.0 / sqrt(sprod), fz = 1.0 / sqrt(zprod);
+    const double fs = rsqrt_nr(sprod), fz = rsqrt_nr(zprod);
     double pn = 0.0;
     for (int i = o + C.lane; i < o + d; i += 64) pn += (z[i] * fz) * (s[i] * fs);
     const double nsum = wave_sum(pn);
     bad |= (1.0 + nsum) < 0.0;
-    const double gamma = sqrt((1.0 + nsum) / 2.0);
+    const double garg = (1.0 + nsum) * 0.5, rg = rsqrt_nr(garg);
+    const double gamma = garg * rg, i2g = 0.5 * rg;  // sqrt((1 + nsum) / 2), 1 / (2 gamma)
     const double s0 = s[o] * fs, z0 = z[o] * fz;
-    const double wb0 = (s0 + z0) / (2.0 * gamma);
+    const double wb0 = (s0 + z0) * i2g;
     double pw = 0.0;
     for (int i = o + 1 + C.lane; i < o + d; i += 64) {
-      const double w = (s[i] * fs - z[i] * fz) / (2.0 * gamma);
+      const double w = (s[i] * fs - z[i] * fz) * i2g;
       wb[i] = w;
       pw += w * w;
     }
     const double wb1sq = wave_sum(pw);
-    const double q = sprod / zprod;
+    const double q = sprod * recip(zprod);
     bad |= q < 0.0;
-    const double rq = sqrt(q);
-    const double mu = sqrt(rq);
-    const double inusq = 1.0 / rq, inu = 1.0 / mu;
-    const double cv = -(1.0 + wb0 + wb1sq / (1.0 + wb0));
-    const double dd = 1.0 + 2.0 / (1.0 + wb0) + wb1sq / ((1.0 + wb0) * (1.0 + wb0));
-    const double av = (wb0 * wb0 + wb1sq - cv * cv * wb1sq / (1.0 + dd * wb1sq)) / 2.0;
+    const double inusq = rsqrt_nr(q), rq = q * inusq;  // 1 / sqrt(q), sqrt(q)
+    const double inu = rsqrt_nr(rq), mu = rq * inu;
+    const double i1 = recip(1.0 + wb0);
+    const double cv = -(1.0 + wb0 + wb1sq * i1);
+    const double dd = 1.0 + 2.0 * i1 + wb1sq * (i1 * i1);
+    const double av = (wb0 * wb0 + wb1sq - cv * cv * wb1sq * recip(1.0 + dd * wb1sq)) * 0.5;
     const double u0a = wb0 * wb0 + wb1sq - av;
     bad |= u0a < 0.0;
-    const double u0 = sqrt(u0a);
-    const double u1 = cv / u0;
+    const double iu0 = rsqrt_nr(u0a), u0 = u0a * iu0;
+    const double u1 = cv * iu0;
     const double v1a = cv * cv / (u0 * u0) - dd;
     bad |= v1a < 0.0;
-    const double v1 = sqrt(v1a);
-    const double tmv1 = sqrt(sqrt(sprod) * sqrt(zprod));
-    const double mult = tmv1 / (z0 + s0 + 2.0 * gamma);
+    const double v1 = sqrt_nr(v1a);
+    const double tmv1 = sqrt_nr((sprod * fs) * (zprod * fz));
+    const double mult = tmv1 * recip(z0 + s0 + 2.0 * gamma);
     for (int i = o + 1 + C.lane; i < o + d; i += 64) {
       D[i] = inusq;
-      iW[i] = sqrt(inusq);
+      iW[i] = inu;  // sqrt(1 / sqrt(q))
       const double wbv = inu * wb[i];
       u[i] = u1 * wbv;
       v[i] = v1 * wbv;
@@ -185,7 +188,7 @@ __device__ __forceinline__ void sqr_scaling_cone(Ctx& C, int c) {
     }
     if (C.lane == 0) {
       D[o] = av * inusq;
-      iW[o] = sqrt(fabs(av * inusq));
+      iW[o] = sqrt_nr(fabs(av * inusq));
       u[o] = inu * u0;
       v[o] = 0.0;
       wb[o] = wb0;

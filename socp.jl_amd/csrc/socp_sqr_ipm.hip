@@ -58,14 +58,15 @@ __device__ void scale_all(const ConeTable& C, const double* wb, const double* mu
   for (int c = 0; c < C.nc; ++c) {
     const int o = C.offs[c], d = C.dim[c];
     if (C.kind[c] == POC_K) {
-      for (int i = o + lane; i < o + d; i += 64) out[i] = inv ? 1.0 / wb[i] * x[i] : wb[i] * x[i];
+      for (int i = o + lane; i < o + d; i += 64) out[i] = inv ? recip(wb[i]) * x[i] : wb[i] * x[i];
       continue;
     }
     double part = 0.0;
     for (int i = o + 1 + lane; i < o + d; i += 64) part += wb[i] * x[i];
     const double del = ws64(part), x0 = x[o], w0 = wb[o];
-    const double cst = inv ? (-x0 + del / (1.0 + w0)) : (x0 + del / (1.0 + w0));
-    const double f = inv ? 1.0 / mu[c] : mu[c];
+    const double iw = recip(1.0 + w0);
+    const double cst = inv ? (-x0 + del * iw) : (x0 + del * iw);
+    const double f = inv ? recip(mu[c]) : mu[c];
     for (int i = o + 1 + lane; i < o + d; i += 64) out[i] = f * (x[i] + cst * wb[i]);
     wsy();
     if (lane == 0) out[o] = inv ? f * (w0 * x0 - del) : f * (w0 * x0 + del);
@@ -82,7 +83,7 @@ __device__ double scmax_w(const ConeTable& C, const double* li, const double* xi
     if (C.kind[c] == POC_K) {
       double v = -INFINITY;
       for (int i = o + lane; i < o + d; i += 64) {
-        const double q = -xi[i] / li[i];
+        const double q = -xi[i] * recip(li[i]);
         if (q > v) v = q;
       }
       val = wm64(v);
@@ -94,15 +95,15 @@ __device__ double scmax_w(const ConeTable& C, const double* li, const double* xi
       }
       const double ai = li[o] * li[o] - ws64(pl);
       dom |= ai < 0.0;
-      const double a = 1.0 / sqrt(ai);
+      const double a = rsqrt_nr(ai);
       const double r1 = a * li[o] * xi[o] - a * ws64(pr);
-      const double cst = (r1 + xi[o]) / (a * li[o] + 1.0);
+      const double cst = (r1 + xi[o]) * recip(a * li[o] + 1.0);
       double r2 = 0.0;
       for (int i = o + 1 + lane; i < o + d; i += 64) {
         const double q = a * (xi[i] - cst * a * li[i]);
         r2 += q * q;
       }
-      val = sqrt(ws64(r2)) - a * r1;
+      val = sqrt_nr(ws64(r2)) - a * r1;
     }
     if (val > mx) mx = val;
   }
@@ -113,7 +114,7 @@ __device__ double scmax_w(const ConeTable& C, const double* li, const double* xi
 __device__ double compute_step_w(const ConeTable& C, const double* l, const double* ds, const double* dz, int lane,
                                  bool& dom) {
   const double t = jmax(jmax(scmax_w(C, l, ds, lane, dom), scmax_w(C, l, dz, lane, dom)), 0.0);
-  return t == 0.0 ? 1.0 : jmin(1.0, 1.0 / t);
+  return t < 1.0 ? 1.0 : (t == INFINITY ? 0.0 : jmin(1.0, recip(t)));  // min(1, 1/t), NaN kept
 }
 
 // max_step (mats.jl:1-28)
@@ -129,7 +130,7 @@ __device__ double max_step_w(const ConeTable& C, const double* x, int lane) {
     } else {
       double sq = 0.0;
       for (int i = o + 1 + lane; i < o + d; i += 64) sq += x[i] * x[i];
-      val = sqrt(ws64(sq)) - x[o];
+      val = sqrt_nr(ws64(sq)) - x[o];
     }
     if (val > mx) mx = val;
   }
