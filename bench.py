@@ -72,6 +72,18 @@ def cone_str(cones):
     return "+".join(out)
 
 
+BASELINE_METRIC = "IPM iters/sec, 65k-batch n=64 dense SOCP at 1/2/4/8 GPU; achieved HBM GB/s"
+
+
+def metric_name(cfg, B):
+    """BASELINE.json's metric for its C2 workload; the same metric named for
+    the other configs' lines (C1, C4 are profile lines, not the headline)."""
+    if cfg.name == "C2" and B == cfg.batch:
+        return BASELINE_METRIC
+    kb = f"{B // 1024}k" if B % 1024 == 0 else str(B)
+    return f"IPM iters/sec, {kb}-batch n={cfg.n} dense SOCP ({cfg.name}); achieved HBM GB/s"
+
+
 def latest_traffic_json(cfg_name):
     """Newest committed PMC traffic summary for the config (profiles/rNN_pmc_traffic[_cfg].json)."""
     import glob
@@ -156,6 +168,24 @@ def cpu_baseline(cfg, fixed_k, budget_s=12.0, threads=None, tol=0.0, structured=
             "sample": f"median of {reps} reps x {chunk} {cfg.name} problems (first {chunk} of the seeded workload), "
                       + (f"tol={tol}, maxit={fixed_k}, " if tol else f"fixed-K={fixed_k}, ")
                       + f"{algo}, OpenMP {threads} threads (OMP_NUM_THREADS / affinity), {total_t:.1f}s timed"}
+
+
+def cpu_allcores(cfg, fixed_k, base, tol=0.0, budget_s=5.0):
+    """The reference-order CPU rate on every CPU of the host, extrapolated: the
+    GPU box gives one GPU's job a 16-CPU share of its cores (OMP_NUM_THREADS),
+    so no run here may use all of them.  The one-thread rate is measured and
+    the line reports nproc x that rate (perfect scaling, an upper bound on
+    what all cores reach) beside the measured per-core rate of the
+    `cpu_baseline` threads -- their ratio is the measured parallel efficiency
+    that the extrapolation assumes to hold up to nproc."""
+    one = cpu_baseline(cfg, fixed_k, budget_s=budget_s, threads=1, tol=tol, reps=3)
+    info = host_cpu_info()
+    ncpu = info["affinity"] or info["nproc"]
+    return {"value": one["value"] * ncpu, "unit": "problem-iterations/s", "cores": ncpu, "kind": "port",
+            "measured": False, "one_thread": one["value"], "per_core_at_threads": base["per_core"],
+            "threads": base["cores"], "efficiency_at_threads": base["per_core"] / one["value"],
+            "sample": f"extrapolated: {ncpu} CPUs x the 1-thread rate ({one['sample']}); not run on all CPUs "
+                      "because the box allots this job OMP_NUM_THREADS of them"}
 
 
 def ingest_line(S, cfg, B, K, tol, dev_data, steps, ctx):
@@ -372,6 +402,9 @@ def main():
                     help="fixed: tol=0, K iterations (headline, SURVEY.md §8(d)(i)); reference: the "
                          "reference's stopping rule, tol=1e-5 absolute, maxit=40, per-problem masking (§8(d)(ii)); "
                          "sqr: the rank-update KKT plugin (socp_sqr_*, spsolver.jl) at the config's shape")
+    ap.add_argument("--explicit-inverse", action="store_true",
+                    help="SOCP_F_EXPLICIT_INVERSE: the reference's operation order (Li = H^-1 formed, "
+                         "densesolver.jl:48) instead of the default H = L L' + triangular solves")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="per CPU line (two lines)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ingest", action="store_true",
@@ -412,7 +445,7 @@ def main():
 
     def solve_shard():
         prev["out"] = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=tol, ctx=ctx,
-                                    out=prev["out"], res=world > 1)
+                                    out=prev["out"], res=world > 1, explicit_inverse=args.explicit_inverse)
         kernel_ms.append(ctx.last_kernel_ms())  # HIP events around the solver launch
         return prev["out"]
 
@@ -432,7 +465,8 @@ def main():
         iters_per_launch = int(out["iters"].sum().item())
         F = flops_per_problem_iter(n, m, k)
         kname = ctx.last_kernel_name()
-        Fx = flops_executed_per_problem_iter(n, m, k, large="large" in kname)
+        Fx = (F if args.explicit_inverse else
+              flops_executed_per_problem_iter(n, m, k, large="large" in kname))
         Bq = bytes_per_problem_iter(n, m, k)
         # binding bound of the algorithmic model: FP64 when F/B is above the
         # ridge (C2, C4), HBM below it (C1)
@@ -452,7 +486,7 @@ def main():
                 traffic = None
         hbm_gbs = traffic / (kms * 1e-3) / 1e9 if traffic else None
         line = {
-            "metric": "IPM iters/sec, 65k-batch n=64 dense SOCP at 1/2/4/8 GPU; achieved HBM GB/s",
+            "metric": metric_name(cfg, B),
             "value": iters_total / dt,
             "unit": "problem-iterations/s",
             "n_gpus": world,
@@ -468,7 +502,10 @@ def main():
                 "workload": f"{cfg.name}: {B} problems per GPU, n={n}, m={m}, k={k}, cones {cone_str(cfg.cones)}, "
                             + (f"initial point + reference stopping rule (tol=1e-5 abs, maxit={K}; "
                                f"value counts executed iterations)" if ref_rule else
-                               f"initial point + fixed-K={K} IPM iterations (tol=0)"),
+                               f"initial point + fixed-K={K} IPM iterations (tol=0)")
+                            + ("; explicit inverse Li = H^-1 (SOCP_F_EXPLICIT_INVERSE, the reference's "
+                               "op order, densesolver.jl:48)" if args.explicit_inverse else ""),
+                "operation_order": "explicit_inverse" if args.explicit_inverse else "cholesky",
                 "global_batch": B * world,
                 "parallelism": f"dp{world} (disjoint problem shards, status all-gather only)",
             },
@@ -496,6 +533,24 @@ def main():
         }
         if world == 1 and not args.no_ingest:
             line["ingest"] = ingest_line(S, cfg, B, K, tol, (c, A, b, G, h), args.steps, ctx)
+        if world == 1 and not args.explicit_inverse and not ref_rule:
+            # the other operation order on the same batch (never `value`): the
+            # reference's explicit Li = H^-1 (SOCP_F_EXPLICIT_INVERSE); its own
+            # line is `--explicit-inverse`
+            xi_ms, xo = [], None
+            for rep in range(1 + args.steps):
+                xo = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=tol, ctx=ctx, out=xo,
+                                   explicit_inverse=True)
+                if rep:
+                    xi_ms.append(ctx.last_kernel_ms())
+            xi_kms = sum(xi_ms) / len(xi_ms)
+            xi_it = int(xo["iters"].sum().item())
+            line["explicit_inverse"] = {
+                "kernel": ctx.last_kernel_name(), "kernel_ms": xi_kms,
+                "value_kernel": xi_it / (xi_kms * 1e-3), "unit": "problem-iterations/s (solver kernel time)",
+                "frac": F * xi_it / (xi_kms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                "mode": "bench.py --explicit-inverse: Li = H^-1 formed by the Gauss-Jordan sweep (densesolver.jl:48), "
+                        "frac by the SURVEY.md §8(d) formula (which this order executes)"}
         if world == 1 and not args.no_ingest and cfg.name == "C2" and not ref_rule:
             # the rank-update plugin (SparseSolver + SqrScaling, socp_sqr_*) at the same shape: its
             # own line is `--mode sqr`; summarised here so every default run records it
@@ -509,6 +564,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol)
             line["cpu_baseline_structured"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol,
                                                            structured=True)
+            line["cpu_baseline_allcores"] = cpu_allcores(cfg, K, line["cpu_baseline"], tol=tol,
+                                                         budget_s=args.cpu_seconds / 2)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

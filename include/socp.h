@@ -114,8 +114,9 @@ int socp_ctx_reset_stream(socp_ctx* ctx);
 /* 1 if a compiled kernel accepts the dims: the register-resident kernel (one
  * wavefront per problem, <= 8 cones, m <= 64; k <= 128 for n <= 48, k <= 96
  * for 48 < n <= 64: the compiled variant table, socp.jl_amd/csrc/gen_inst.py)
- * or the blocked kernel (n, m <= 512, <= 64 cones, any k; one 512-thread
- * workgroup per problem), which also takes every register-kernel shape.  The
+ * or the blocked kernel (n, m <= 512, <= 64 cones, k <= 2^21 -- its LDS /
+ * vector offsets are 32-bit; one 512-thread workgroup per problem), which also
+ * takes every register-kernel shape.  The
  * blocked kernel keeps the problem's vectors in the 160 KiB LDS of a CU when
  * they fit (C4, n=512 m=64 k=640, uses 126 KiB) and in its HBM workspace slot
  * otherwise (e.g. k = 1000 at n = 512).  Other shapes return
@@ -273,7 +274,9 @@ int socp_sqr_scaling(socp_sqr* h, double* l, double* wbs, double* mu);
  * NULL) out.  params NULL: socp_params_default.  Host or device pointers as
  * the handle's flags.  Afterwards the records hold the last factorisation.
  * With tol > 0 the call synchronises its stream every 4 iterations to stop
- * launching once every problem has stopped (converged or failed).
+ * launching once every problem has stopped (converged or failed); such a call
+ * cannot be captured into a HIP graph.  With tol <= 0 (fixed iteration count)
+ * it issues only stream-ordered work until the final copies.
  * The initial point factors G'G (+ A'A where sing) with W = I: `sing` must be
  * the flag Problem() computes (Socp.jl:49-56, cholesky(G'G) fails).  Where the
  * given flag disagrees and that factorisation fails, the problem stops with

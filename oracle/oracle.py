@@ -19,7 +19,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+# SOCP_ORACLE_LIB: another build of the same source (e.g. build/liboracle_asan.so, `make asan-test`)
+_LIB_PATH = os.environ.get("SOCP_ORACLE_LIB") or os.path.join(_HERE, "build", "liboracle.so")
 
 POC, SOC = 0, 1
 

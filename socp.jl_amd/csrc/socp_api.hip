@@ -228,6 +228,16 @@ static const SmallVariant* pick_variant(int n, int m, int k) {
 // they fit; otherwise (e.g. k = 1000 at n = 512) in the workgroup's slot of the
 // HBM workspace (*gv: the GV kernels), with only the problem index in LDS.
 static bool large_fits(int n, int m, int k, int nc, size_t* lds_bytes, bool* gv = nullptr) {
+  // Every LDS / vector offset of the kernel (LargeLayout::o_*, total, LV(int))
+  // is a 32-bit int and X = W^-1 G (KP x NPAD) is addressed from int row
+  // offsets: bound k before the layout is computed in int, so that neither
+  // wraps (the layout's size is computed here in int64).
+  if (n < 0 || m < 0 || k < 0 || k > LARGE_KMAX) return false;
+  {
+    const int64_t KP = ((int64_t)k + 15) / 16 * 16, RW = 512;
+    const int64_t lds_total = 16 * KP + 2 * RW + 1024 + 64 + 8 * RW + 16 * RW + 12 * MAXC + 6 * RW + 5 * RW + 64 + 512;
+    if (lds_total > INT32_MAX / 2 || KP * RW > INT32_MAX) return false;
+  }
   const LargeLayout L = large_layout(n, m, k);
   if (L.NPAD > 64 * LARGE_NB_MAX || L.MPAD > 64 * LARGE_NB_MAX || nc > MAXC) return false;
   size_t lds = (size_t)L.total * sizeof(double);
@@ -246,7 +256,7 @@ extern "C" int socp_supported(const socp_dims* d) {
 
 static const char* kUnsupported =
     "dims outside both kernels (register-resident: n, m <= 64, k <= 128, <= 8 cones; "
-    "blocked: n, m <= 512, <= 64 cones)";
+    "blocked: n, m <= 512, <= 64 cones, k <= 2^21)";
 
 // ---------------------------------------------------------------- launch
 static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_DIAG builds)
@@ -1064,11 +1074,8 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
   ia.status = ip; ia.iters = ip + B; ia.active = ip + 2 * B; ia.st_setup = ip + 3 * B;
   int32_t* st_solve = ip + 4 * B;
   ia.n_active = ip + 5 * B;
-  {
-    const int32_t nb = (int32_t)B;
-    HIPCHK(hipMemcpyAsync(ia.n_active, &nb, sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));  // nb is a stack value
-  }
+  // the active count starts at B, set on the stream (no host round trip)
+  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)ia.n_active, (int)B, 1, ctx->stream));
   const bool dev = h->dev;
   if (dev) {
     ia.c = c; ia.b = m ? b : nullptr; ia.h = hv;

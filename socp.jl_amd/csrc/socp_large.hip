@@ -2234,7 +2234,7 @@ struct Large {
     BAR();
     LSTAMP(SP_STORE);
 #ifdef SOCP_DIAG
-    if (tid == 0) reinterpret_cast<unsigned long long*>(lg_lds + L.o_red + 16)[NSTAMP] += iters;
+    if (!GV && tid == 0) reinterpret_cast<unsigned long long*>(lg_lds + L.o_red + 16)[NSTAMP] += iters;
 #endif
   }
 };

@@ -472,13 +472,20 @@ __device__ __forceinline__ double ipow(double x, int e) {
   return r;
 }
 
-// pivot reciprocal: v_rcp_f64 + two Newton steps (within 1 ulp of 1/d)
+// IEEE classes (v_cmp_class_f64 mask bits) at which the Newton refinement of
+// a v_rcp / v_rsq seed would turn an exact 0 or inf into NaN (0 * inf): +-0,
+// +-inf.  There the seed is the IEEE result itself and is returned as is.
+constexpr int kClassZeroInf = (1 << 2) | (1 << 5) | (1 << 6) | (1 << 9);
+
+// pivot reciprocal: v_rcp_f64 + two Newton steps (within 1 ulp of 1/d; 1/+-0 =
+// +-inf and 1/+-inf = +-0 exactly, as IEEE division gives)
 __device__ __forceinline__ double recip(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  double e = fma(-d, r, 1.0);
-  r = fma(r, e, r);
+  const double r0 = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r0, 1.0);
+  double r = fma(r0, e, r0);
   e = fma(-d, r, 1.0);
-  return fma(r, e, r);
+  r = fma(r, e, r);
+  return __builtin_amdgcn_class(d, kClassZeroInf) ? r0 : r;
 }
 
 // Reduce-scatter over the 16 lanes of a row (xor masks 8,4,2,1): on return the
@@ -563,14 +570,16 @@ __device__ __forceinline__ void row_bcast4(double x, double (&out)[4]) {
   }
 }
 
-// x^-1/2: v_rsq_f64 + two Newton steps (within 1 ulp)
+// x^-1/2: v_rsq_f64 + two Newton steps (within 1 ulp; +-0 -> +-inf and
+// +inf -> 0 as 1/sqrt gives them in IEEE arithmetic, negative -> NaN)
 __device__ __forceinline__ double rsqrt_nr(double d) {
-  double y = __builtin_amdgcn_rsq(d);
+  const double y0 = __builtin_amdgcn_rsq(d);
   const double h = 0.5 * d;
-  double e = fma(-(h * y), y, 0.5);
-  y = fma(y, e, y);
+  double e = fma(-(h * y0), y0, 0.5);
+  double y = fma(y0, e, y0);
   e = fma(-(h * y), y, 0.5);
-  return fma(y, e, y);
+  y = fma(y, e, y);
+  return __builtin_amdgcn_class(d, kClassZeroInf) ? y0 : y;
 }
 // square root through rsqrt_nr (0 and +inf passed through, negative -> NaN)
 __device__ __forceinline__ double sqrt_nr(double d) {
@@ -2428,46 +2437,6 @@ struct Small {
     SYNC();
   }
 
-  // gemv_G and gemv_Gt in one pass over G (the residuals' Gx and G'z): each
-  // G element is copied out of its AGPRs once for both products; the
-  // accumulation orders are gemv_G's and gemv_Gt's, so the results are theirs
-  // bit for bit.  acc: lane partials of G'v (rows_sum'd by the caller).
-  template <int P0, int CH>
-  __device__ __forceinline__ void gemv_G2_chunk(const double (&uq)[NQ], double (&acc)[NQ], int v, int add1, int add2,
-                                                int out) {
-    LANE_IDS();
-    double P[CH];
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      const double vp = LDS(v + 4 * (P0 + j) + g);
-      double s = 0.0;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const double gq = a_get(G[P0 + j][q]);
-        s = fma(gq, uq[q], s);
-        acc[q] = fma(gq, vp, acc[q]);
-      }
-      P[j] = s;
-    }
-    int base = 0;
-    rs16<CH, 8>(P, cl, base);
-    constexpr int CF = RSCount<CH, 8>::value;
-#pragma unroll
-    for (int j = 0; j < CF; ++j) {
-      const int row = 4 * (P0 + base + j) + g;
-      if (row < k) {
-        double w = P[j];
-        if (add1 >= 0) w = w + LDS(add1 + row);
-        w = w - LDS(add2 + row);
-        LDS(out + row) = w;
-      }
-    }
-    if constexpr (P0 + CH < NP) {
-      constexpr int NXT = (NP - P0 - CH) < 8 ? (NP - P0 - CH) : 8;
-      gemv_G2_chunk<P0 + CH, NXT>(uq, acc, v, add1, add2, out);
-    }
-  }
-
   // acc[q] (all lanes) = (G' v)[16q+cl].  The v reads of the next batch of
   // row steps are issued before the current batch's products (one exposed
   // LDS round trip per call, not one per pair of row steps).
@@ -2627,28 +2596,11 @@ struct Small {
       zv[t] = LDS(Z_ + 64 * t + lane);
       sv[t] = LDS(S_ + 64 * t + lane);
     }
-#ifndef SOCP_RESID_MERGE
-#define SOCP_RESID_MERGE 0
-#endif
-#if SOCP_RESID_MERGE
-    {  // G'z and Gx + s - h in one pass over G
-      double uq[NQ];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        uq[q] = LDS(X_ + 16 * q + cl);
-        acc[q] = 0.0;
-      }
-      gemv_G2_chunk<0, (NP < 8 ? NP : 8)>(uq, acc, Z_, S_, H_, DZ);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) acc[q] = rows_sum(acc[q]);
-    }
-#else
     if (SOCP_KO & 32) {
       for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
     } else {
       gemv_Gt(Z_, acc);
     }
-#endif
     if (SOCP_KO & 128) {
       for (int q = 0; q < NQ; ++q) at[q] = 0.0;
     } else {
@@ -2667,11 +2619,7 @@ struct Small {
       }
     }
     const double p2 = (SOCP_KO & 128) ? 0.0 : A_mv(X_, B_, RP, O_A, true);
-#if SOCP_RESID_MERGE
-    SYNC();
-#else
     if (!(SOCP_KO & 16)) gemv_G_r<true>(xq, S_, H_, DZ);
-#endif
 #pragma unroll
     for (int t = 0; t < NS; ++t)
       if (64 * t + lane < k) zs += zv[t] * sv[t];

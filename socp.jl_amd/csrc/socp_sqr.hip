@@ -224,13 +224,14 @@ __device__ __forceinline__ double dot_strided(const double* p, int64_t stride, c
 #endif
 
 // 1/sqrt(x) from v_rsq_f64 refined by two Newton steps (to within an ulp or
-// two; x <= 0 or NaN gives NaN or inf, which the callers' status checks catch)
+// two; x < 0 or NaN gives NaN, which the callers' status checks catch; +-0 and
+// +inf give the IEEE +-inf and 0, not the 0 * inf NaN of the refinement)
 __device__ __forceinline__ double rsqrt_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
+  const double y0 = __builtin_amdgcn_rsq(x);
   const double hx = 0.5 * x;
+  double y = y0 * (1.5 - hx * y0 * y0);
   y = y * (1.5 - hx * y * y);
-  y = y * (1.5 - hx * y * y);
-  return y;
+  return __builtin_amdgcn_class(x, kClassZeroInf) ? y0 : y;
 }
 
 // ------------------------------------------------------------ factor ops

@@ -72,7 +72,8 @@ def main():
         out["cases"].append(case(name, cones, c, A, b, G, h, 12, {"kats": name}))
     # C4 (n=512): its bench K=5 iterations, 4 problems (the
     # blocked kernel's configuration)
-    for cfg, count, iters in ((C0B, 4, 6), (C1, 8, 4), (C2, 4, 7), (C4, 4, 5)):
+    # C2: its bench K=8 iterations (the trajectory gates cover every iteration the bench times)
+    for cfg, count, iters in ((C0B, 4, 6), (C1, 8, 4), (C2, 8, 8), (C4, 4, 5)):
         d = O.generate(cfg.cones, count, cfg.n, cfg.m, cfg.k, cfg.seed)
         for p in range(count):
             c = d["c"][p * cfg.n:(p + 1) * cfg.n]

@@ -50,8 +50,11 @@ def test_supported_dims():
     for n, m, k, nc in ((600, 0, 601, 1), (64, 600, 128, 1), (256, 0, 130, 65)):
         assert not L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
     # k-vectors over the 160 KiB LDS run with the vectors in HBM (the GV kernels)
-    for n, m, k, nc in ((512, 64, 1000, 8), (64, 16, 4096, 4)):
+    for n, m, k, nc in ((512, 64, 1000, 8), (64, 16, 4096, 4), (64, 16, 1 << 21, 4)):
         assert L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
+    # beyond the blocked kernel's 32-bit LDS / vector offsets (LARGE_KMAX)
+    for n, m, k, nc in ((64, 16, (1 << 21) + 1, 4), (512, 64, 1 << 30, 8), (8, 0, 2**31 - 1, 1)):
+        assert not L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
 
 
 def test_null_context_is_an_api_error():

@@ -1,23 +1,36 @@
 #!/bin/bash
-# Round measurement session: GPU tests, smoke, bench lines (C2 headline, C4),
-# rocprofv3 kernel stats, PMC HBM traffic passes (one counter per pass),
-# phase stamps.  Each GPU step has its own limit; the first failure ends it.
+# Round-4 measurement session: PMC HBM traffic (FETCH_SIZE, WRITE_SIZE, one
+# counter per pass) for C2 / C4 / C1, SQ issue/stall counters of the C2
+# kernel, rocprofv3 kernel stats of each config's bench command, then the
+# bench lines against the fresh traffic files (copied to profiles/ by hand).
 set -e
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-tail -2 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -30 gpurun_out/smoke.log; exit 1; }
-tail -1 gpurun_out/smoke.log
-timeout -k 10 400 python bench.py > gpurun_out/bench_c2.json.log 2>&1 || { tail -30 gpurun_out/bench_c2.json.log; exit 1; }
-timeout -k 10 400 python bench.py --config C4 --steps 3 --warmup 1 --traffic-json profiles/r01_pmc_traffic_c4.json > gpurun_out/bench_c4.json.log 2>&1 || { tail -30 gpurun_out/bench_c4.json.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c2 -o c2 -- python bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof_c2.log 2>&1 || { tail -30 gpurun_out/prof_c2.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 -o c4 -- python bench.py --config C4 --steps 3 --warmup 1 --no-cpu > gpurun_out/prof_c4.log 2>&1 || { tail -30 gpurun_out/prof_c4.log; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o f -- python bench.py --steps 1 --warmup 0 --no-cpu > gpurun_out/pmc_fetch.log 2>&1 || { tail -30 gpurun_out/pmc_fetch.log; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o w -- python bench.py --steps 1 --warmup 0 --no-cpu > gpurun_out/pmc_write.log 2>&1 || { tail -30 gpurun_out/pmc_write.log; exit 1; }
-python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write C2 65536 8 gpurun_out/pmc_traffic.json
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch4 -o f -- python bench.py --config C4 --steps 1 --warmup 0 --no-cpu > gpurun_out/pmc_fetch4.log 2>&1 || { tail -30 gpurun_out/pmc_fetch4.log; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write4 -o w -- python bench.py --config C4 --steps 1 --warmup 0 --no-cpu > gpurun_out/pmc_write4.log 2>&1 || { tail -30 gpurun_out/pmc_write4.log; exit 1; }
-python tools/pmc_traffic.py gpurun_out/pmc_fetch4 gpurun_out/pmc_write4 C4 1024 5 gpurun_out/pmc_traffic_c4.json
-timeout -k 10 300 python tools/stamps.py C2,C1,C4 > gpurun_out/stamps.log 2>&1 || { tail -30 gpurun_out/stamps.log; exit 1; }
-cat gpurun_out/pmc_traffic.json gpurun_out/pmc_traffic_c4.json
+O=gpurun_out/r04m
+mkdir -p $O
+pmc() {  # name config batch K suffix
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_f_$1 -o f -- python3 bench.py --config $2 --steps 1 --warmup 0 --no-cpu --no-ingest > $O/pmc_f_$1.log 2>&1 || { tail -20 $O/pmc_f_$1.log; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_w_$1 -o w -- python3 bench.py --config $2 --steps 1 --warmup 0 --no-cpu --no-ingest > $O/pmc_w_$1.log 2>&1 || { tail -20 $O/pmc_w_$1.log; exit 1; }
+  python3 tools/pmc_traffic.py $O/pmc_f_$1 $O/pmc_w_$1 $2 $3 $4 $O/pmc_traffic$5.json
+}
+pmc c2 C2 65536 8 ""
+pmc c4 C4 1024 5 "_c4"
+pmc c1 C1 4096 3 "_c1"
+echo "pmc done"
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES --output-format csv -d $O/sq1 -o p1 -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-ingest > $O/sq1.log 2>&1 || { tail -20 $O/sq1.log; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD --output-format csv -d $O/sq2 -o p2 -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-ingest > $O/sq2.log 2>&1 || { tail -20 $O/sq2.log; exit 1; }
+echo "sq done"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c2 -o c2 -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-ingest > $O/prof_c2.log 2>&1 || { tail -30 $O/prof_c2.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4 -o c4 -- python3 bench.py --config C4 --steps 3 --warmup 1 --no-cpu --no-ingest > $O/prof_c4.log 2>&1 || { tail -30 $O/prof_c4.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c1 -o c1 -- python3 bench.py --config C1 --steps 5 --warmup 2 --no-cpu --no-ingest > $O/prof_c1.log 2>&1 || { tail -30 $O/prof_c1.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_sqr -o sqr -- python3 bench.py --mode sqr --steps 3 --warmup 1 --no-cpu > $O/prof_sqr.log 2>&1 || { tail -30 $O/prof_sqr.log; exit 1; }
+echo "prof done"
+timeout -k 10 500 python3 bench.py --traffic-json $O/pmc_traffic.json > $O/bench_c2.log 2>&1 || { tail -30 $O/bench_c2.log; exit 1; }
+grep '^{' $O/bench_c2.log | cut -c1-300
+timeout -k 10 400 python3 bench.py --config C4 --steps 3 --warmup 1 --no-ingest --traffic-json $O/pmc_traffic_c4.json > $O/bench_c4.log 2>&1 || { tail -30 $O/bench_c4.log; exit 1; }
+grep '^{' $O/bench_c4.log | cut -c1-300
+timeout -k 10 300 python3 bench.py --config C1 --no-ingest --traffic-json $O/pmc_traffic_c1.json > $O/bench_c1.log 2>&1 || { tail -30 $O/bench_c1.log; exit 1; }
+grep '^{' $O/bench_c1.log | cut -c1-300
+timeout -k 10 400 python3 bench.py --mode reference --no-ingest > $O/bench_refrule.log 2>&1 || { tail -30 $O/bench_refrule.log; exit 1; }
+grep '^{' $O/bench_refrule.log | cut -c1-300
+timeout -k 10 400 python3 bench.py --mode sqr --steps 10 --warmup 2 > $O/bench_sqr.log 2>&1 || { tail -30 $O/bench_sqr.log; exit 1; }
+grep '^{' $O/bench_sqr.log | cut -c1-300
