@@ -581,6 +581,10 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
   y = fma(y, e, y);
   return __builtin_amdgcn_class(d, kClassZeroInf) ? y0 : y;
 }
+// x * q for q = rsqrt_nr(p) where p = 0 makes q = inf: an exact zero factor
+// stays zero, as sqrt(0 * y) and sqrt(0 / y) are in IEEE arithmetic (a
+// boundary iterate of a POC cone, s_i z_i = 0), instead of 0 * inf = NaN
+__device__ __forceinline__ double zmul(double x, double q) { return x == 0.0 ? x : x * q; }
 // square root through rsqrt_nr (0 and +inf passed through, negative -> NaN)
 __device__ __forceinline__ double sqrt_nr(double d) {
   const double r = d * rsqrt_nr(d);
@@ -1196,12 +1200,12 @@ struct Small {
       const double wt = si[s] * as - zi[s] * az;
       const double lt = si[s] * bs + zi[s] * bz;
       dm = dm || (poc && pr < 0.0);
-      wbi[s] = poc ? si[s] * q : (tail ? wt : ccv(CC_WB0, c));
-      li[s] = poc ? pr * q : (tail ? lt : l0);
+      wbi[s] = poc ? zmul(si[s], q) : (tail ? wt : ccv(CC_WB0, c));
+      li[s] = poc ? zmul(pr, q) : (tail ? lt : l0);
       if (poc || tail) {
         LDS(WB + i) = wbi[s];
         LDS(LAM + i) = li[s];
-        LDS(CA + i) = poc ? zi[s] * q : imu;
+        LDS(CA + i) = poc ? zmul(zi[s], q) : imu;
         LDS(CBV + i) = poc ? 0.0 : wt * imu;
         if (poc) LDS(IL + i) = q;
         if (write_ds) LDS(DS + i) = -(poc ? li[s] * li[s] : (l0 * li[s] + l0 * li[s]));  // -ds: the RHS

@@ -130,9 +130,9 @@ __device__ __forceinline__ void sqr_scaling_cone(Ctx& C, int c) {
       const double sz = s[i] * z[i], q = rsqrt_nr(sz);
       bad |= sz < 0.0;
       D[i] = z[i] * recip(s[i]);
-      iW[i] = z[i] * q;
-      lam[i] = sz * q;
-      wb[i] = s[i] * q;
+      iW[i] = zmul(z[i], q);  // s z = 0 (a boundary iterate): q = inf, the zero factors stay 0 as in IEEE sqrt
+      lam[i] = zmul(sz, q);
+      wb[i] = zmul(s[i], q);
       u[i] = 0.0;
       v[i] = 0.0;
     }
@@ -591,12 +591,15 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
       const int i = e % m, j = e / m;
       rec[L.r_S + e] = i >= j ? Sm[j * L.ldm + i] : 0.0;
     }
-    for (int i = lane; i < k; i += 64) {
-      rec[L.r_l + i] = lds[L.o_l + i];
-      rec[L.r_wb + i] = lds[L.o_wb + i];
-    }
-    for (int c = lane; c < nc; c += 64) rec[L.r_mu + c] = lds[L.o_mu + c];
   }
+  // the scaling whatever the factorisation did: compute_scaling runs (and
+  // updates the SqrScaling object) before setup_iter's cholesky! can throw
+  // (solver.jl:106,126)
+  for (int i = lane; i < k; i += 64) {
+    rec[L.r_l + i] = lds[L.o_l + i];
+    rec[L.r_wb + i] = lds[L.o_wb + i];
+  }
+  for (int c = lane; c < nc; c += 64) rec[L.r_mu + c] = lds[L.o_mu + c];
   if (lane == 0) {
     rec[L.r_st] = (double)status;
     a.status[p] = status;
@@ -988,12 +991,14 @@ __device__ __forceinline__ void setup_problem_wg(Ctx& C, int64_t p, int tid) {
           rec[L.r_S + e] = i >= j ? P[sqr_pk(i, j, m)] : 0.0;
         }
     }
-    for (int i = tid; i < k; i += SQR_LT) {
-      rec[L.r_l + i] = lds[L.o_l + i];
-      rec[L.r_wb + i] = lds[L.o_wb + i];
-    }
-    for (int c = tid; c < nc; c += SQR_LT) rec[L.r_mu + c] = lds[L.o_mu + c];
   }
+  // the scaling whatever the factorisation did (compute_scaling precedes
+  // setup_iter's cholesky!, solver.jl:106,126)
+  for (int i = tid; i < k; i += SQR_LT) {
+    rec[L.r_l + i] = lds[L.o_l + i];
+    rec[L.r_wb + i] = lds[L.o_wb + i];
+  }
+  for (int c = tid; c < nc; c += SQR_LT) rec[L.r_mu + c] = lds[L.o_mu + c];
   if (tid == 0) {
     rec[L.r_st] = (double)status;
     a.status[p] = status;

@@ -39,8 +39,11 @@ from socp_amd.configs import C2
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# explicit-inverse gates (provisional until measured on MI355X)
-XI_GATES = dict(conv_slack=0.02, same=0.85, of_conv=0.95, iters1=0.90)
+# explicit-inverse gates, a few points inside the values measured on MI355X
+# (hip_xi [3483, 3, 505, 0, 105] vs structured [3337, 2, 652, 0, 105]: the same
+# outcome on 85.6 %, of its converged HIP converges on 95.1 %, where both
+# converge |d iters| <= 1 on 99.7 %)
+XI_GATES = dict(conv_slack=0.01, same=0.83, of_conv=0.93, iters1=0.98)
 
 
 def _arr(s, dt):

@@ -492,3 +492,47 @@ def test_sqr_solve_socp_isolation_and_device(oracle):
     torch.cuda.synchronize()
     for key in ("x", "y", "z", "s", "iters", "status", "res"):
         assert np.array_equal(gd[key].cpu().numpy(), clean[key]), key
+
+
+def test_scaling_at_a_boundary_iterate(kats, oracle):
+    """A POC element on the cone boundary (s_i z_i = 0): the square roots of
+    the scaling come from one Newton-refined 1/sqrt(s z), which is inf there;
+    the reference's IEEE sqrt gives lambda_i = sqrt(s z) = 0 and
+    wbs_i = sqrt(s/z) = 0 (s_i = 0) or inf (z_i = 0), and so must the device
+    (not 0 * inf = NaN).  The other entries stay within 1e-12 of the oracle.
+    Both plugins then report the factorisation failure where the reference's
+    cholesky! throws (W^-2 has an infinite entry): status 2."""
+    q = kats["sqr_scaling"]
+    cones = [tuple(c) for c in q["cones"]]
+    assert cones[0][0] == 0  # a POC block first
+    G = np.array(q["G"], dtype=np.float64)
+    k, n = G.shape
+    s0, z0 = np.array(q["pairs"][0]["s"], float), np.array(q["pairs"][0]["z"], float)
+    s1, z1 = s0.copy(), z0.copy()
+    s1[0] = 0.0  # lambda_0 = 0, wbs_0 = 0
+    s2, z2 = s0.copy(), z0.copy()
+    z2[0] = 0.0  # lambda_0 = 0, wbs_0 = inf
+    S_, Z_ = [s1, s2], [z1, z2]
+    B = 2
+    h = S.SqrHandle(cones, n, 0, k, None, np.tile(G.ravel(order="F"), B))
+    st = h.setup_iter(np.concatenate(S_), np.concatenate(Z_))
+    sc = h.scaling()
+    for p in range(B):
+        ref = oracle.compute_scaling(cones, S_[p], Z_[p])
+        for key in ("l", "wbs"):
+            got, want = np.asarray(sc[key][p]), np.asarray(ref[key])
+            assert got[0] == want[0], (p, key, got, want)  # the boundary element: 0 or inf exactly
+            assert np.abs(got[1:] - want[1:]).max() < 1e-12, (p, key, got, want)
+    # the factorisation outcome as the oracle's (s_0 = 0: W^-2 has an infinite
+    # entry, cholesky! throws; z_0 = 0: that row drops out of H), for both plugins
+    zr = lambda q: np.zeros(q)  # noqa: E731
+    A0 = np.zeros((0, n))
+    want_sqr = [oracle.sqr_kkt_single(cones, A0, G, False, S_[p], Z_[p], zr(n), zr(0), zr(k), zr(k))["status"]
+                for p in range(B)]
+    want_dense = [oracle.kkt_single(cones, A0, G, False, S_[p], Z_[p], zr(n), zr(0), zr(k), zr(k))["status"]
+                  for p in range(B)]
+    assert want_sqr[0] == 2 and want_dense[0] == 2, (want_sqr, want_dense)
+    assert st.tolist() == want_sqr, (st, want_sqr)
+    d = S.DenseHandle(cones, n, 0, k, None, np.tile(G.ravel(order="F"), B))
+    assert d.setup_iter(np.concatenate(S_), np.concatenate(Z_)).tolist() == want_dense
+    d.close()
