@@ -611,6 +611,9 @@ __device__ __forceinline__ double rsqrt_tile(double d) {
 #ifndef SOCP_TRANSPOSE_MFMA
 #define SOCP_TRANSPOSE_MFMA 0
 #endif
+#ifndef SOCP_TILE_OKDIAG
+#define SOCP_TILE_OKDIAG 0  // 1: the pivot test once per tile, on the diagonal of W
+#endif
 #ifndef SOCP_TILE_INPLACE
 #define SOCP_TILE_INPLACE 1  // 0: copy back only registers > B (A/B builds)
 #endif
@@ -679,7 +682,9 @@ __device__ __forceinline__ void tile_block(d4& Dt, d4& It, d4& W, bool& ok, cons
       const double r23 = fma(-r12, r13, fma(-r02, r03, a23)) * rs2;
       const double s33 = fma(-r23, r23, fma(-r13, r13, fma(-r03, r03, a33)));
       const double rs3 = rsqrt_tile(s33);
+#if !SOCP_TILE_OKDIAG
       ok = ok && (a00 > 0.0) && (s11 > 0.0) && (s22 > 0.0) && (s33 > 0.0);  // NaN fails too
+#endif
       double V[4], X[4];
       row_bcast4(v, V);
       row_bcast4(w, X);
@@ -727,6 +732,15 @@ __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok, const H& hoo
   for (int r = 0; r < 4; ++r) It[r] = (g + 4 * r == cl) ? 1.0 : 0.0;
   W = It;
   tile_block<0, INPL>(Dt, It, W, ok, hook);
+#if SOCP_TILE_OKDIAG
+  // potrf's test once per tile: the diagonal of W = L^-1 holds the pivots'
+  // 1/sqrt, which is finite and > 0 exactly when every pivot is > 0 (a pivot
+  // <= 0 or NaN makes rsqrt_tile NaN; a NaN anywhere reaches every later pivot)
+  bool dg = true;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dg = dg && (g + 4 * r != cl || W[r] > 0.0);
+  ok = ok && __all(dg);
+#endif
 }
 
 
