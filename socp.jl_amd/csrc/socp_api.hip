@@ -227,19 +227,23 @@ static const SmallVariant* pick_variant(int n, int m, int k) {
 // in registers).  The problem's vectors live in the 160 KiB LDS of a CU when
 // they fit; otherwise (e.g. k = 1000 at n = 512) in the workgroup's slot of the
 // HBM workspace (*gv: the GV kernels), with only the problem index in LDS.
-static bool large_fits(int n, int m, int k, int nc, size_t* lds_bytes, bool* gv = nullptr) {
+static bool large_fits(int n, int m, int k, int nc, size_t* lds_bytes, bool* gv = nullptr, bool xi = false) {
   // Every LDS / vector offset of the kernel (LargeLayout::o_*, total, LV(int))
   // is a 32-bit int and X = W^-1 G (KP x NPAD) is addressed from int row
   // offsets: bound k before the layout is computed in int, so that neither
   // wraps (the layout's size is computed here in int64).
   if (n < 0 || m < 0 || k < 0 || k > LARGE_KMAX) return false;
   {
-    const int64_t KP = ((int64_t)k + 15) / 16 * 16, RW = 512;
+    const int64_t KP = ((int64_t)k + 15) / 16 * 16, NP = ((int64_t)n + 63) / 64 * 64,
+                  MP = ((int64_t)(m > 0 ? m : 1) + 63) / 64 * 64, RW = NP > MP ? NP : MP;
     const int64_t lds_total = 16 * KP + 2 * RW + 1024 + 64 + 8 * RW + 16 * RW + 12 * MAXC + 6 * RW + 5 * RW + 64 + 512;
     if (lds_total > INT32_MAX / 2 || KP * RW > INT32_MAX) return false;
   }
   const LargeLayout L = large_layout(n, m, k);
-  if (L.NPAD > 64 * LARGE_NB_MAX || L.MPAD > 64 * LARGE_NB_MAX || nc > MAXC) return false;
+  // n: up to 64 LARGE_NB_MAX_CHOL with the Cholesky factor (wide panels in
+  // windows, socp_large.hip panel_chol_wide), 64 LARGE_NB_MAX where H is swept
+  // (SOCP_F_EXPLICIT_INVERSE: a panel row in registers); m: S is always swept
+  if (L.NPAD > 64 * (xi ? LARGE_NB_MAX : LARGE_NB_MAX_CHOL) || L.MPAD > 64 * LARGE_NB_MAX || nc > MAXC) return false;
   size_t lds = (size_t)L.total * sizeof(double);
   const bool g = lds + 64 > 160 * 1024;
   if (g) lds = 64 * sizeof(double);
@@ -256,7 +260,7 @@ extern "C" int socp_supported(const socp_dims* d) {
 
 static const char* kUnsupported =
     "dims outside both kernels (register-resident: n, m <= 64, k <= 128, <= 8 cones; "
-    "blocked: n, m <= 512, <= 64 cones, k <= 2^21)";
+    "blocked: n <= 2048 (512 with SOCP_F_EXPLICIT_INVERSE), m <= 512, <= 64 cones, k <= 2^21)";
 
 // ---------------------------------------------------------------- launch
 static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_DIAG builds)
@@ -300,8 +304,8 @@ static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
 static int launch_large(socp_ctx* ctx, const SmallArgs& a, double* rec = nullptr) {
   size_t lds = 0;
   bool gv = false;
-  if (!large_fits(a.n, a.m, a.k, a.nc, &lds, &gv)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
   const bool xi = (a.flags & SOCP_F_EXPLICIT_INVERSE) != 0;
+  if (!large_fits(a.n, a.m, a.k, a.nc, &lds, &gv, xi)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
   const void* kern = large_kernel_ptr(xi, gv);
   HIPCHK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = 0;
@@ -456,7 +460,8 @@ extern "C" int socp_batch_solve_ex(socp_ctx* ctx, const socp_dims* dims, const i
     return fail(SOCP_E_INVALID, "NULL data pointer");
   const bool force_large = (P.flags & SOCP_F_FORCE_LARGE) != 0;
   const SmallVariant* v = (force_large || dims->ncones > NCS) ? nullptr : pick_variant(n, m, k);
-  if (!v && !large_fits(n, m, k, dims->ncones, nullptr)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
+  if (!v && !large_fits(n, m, k, dims->ncones, nullptr, nullptr, (P.flags & SOCP_F_EXPLICIT_INVERSE) != 0))
+    return fail(SOCP_E_UNSUPPORTED, kUnsupported);
   HIPCHK(hipSetDevice(ctx->device));
   const bool dev = (P.flags & SOCP_F_DEVICE_PTRS) != 0;
   const bool warm = (P.flags & SOCP_F_WARM_START) != 0;
@@ -552,7 +557,8 @@ extern "C" int socp_batch_kkt_solve(socp_ctx* ctx, const socp_dims* dims, const 
     return fail(SOCP_E_INVALID, "NULL data pointer");
   const bool force_large = (flags & SOCP_F_FORCE_LARGE) != 0;
   const SmallVariant* v = (force_large || dims->ncones > NCS) ? nullptr : pick_variant(n, m, k);
-  if (!v && !large_fits(n, m, k, dims->ncones, nullptr)) return fail(SOCP_E_UNSUPPORTED, kUnsupported);
+  if (!v && !large_fits(n, m, k, dims->ncones, nullptr, nullptr, (flags & SOCP_F_EXPLICIT_INVERSE) != 0))
+    return fail(SOCP_E_UNSUPPORTED, kUnsupported);
   HIPCHK(hipSetDevice(ctx->device));
   const bool dev = (flags & SOCP_F_DEVICE_PTRS) != 0;
   a.B = B;
@@ -679,7 +685,8 @@ extern "C" int socp_dense_create(socp_ctx* ctx, const socp_dims* dims, const int
   if (B > 0 && (!G || (m > 0 && !A))) return bail(fail(SOCP_E_INVALID, "NULL data pointer"));
   const bool force_large = (flags & SOCP_F_FORCE_LARGE) != 0;
   h->v = (force_large || dims->ncones > NCS) ? nullptr : pick_variant(n, m, k);
-  if (!h->v && !large_fits(n, m, k, dims->ncones, nullptr)) return bail(fail(SOCP_E_UNSUPPORTED, kUnsupported));
+  if (!h->v && !large_fits(n, m, k, dims->ncones, nullptr, nullptr, (flags & SOCP_F_EXPLICIT_INVERSE) != 0))
+    return bail(fail(SOCP_E_UNSUPPORTED, kUnsupported));
   if (hipSetDevice(ctx->device) != hipSuccess) return bail(fail(SOCP_E_HIP, "hipSetDevice"));
   const bool dev = (flags & SOCP_F_DEVICE_PTRS) != 0;
   a.B = B;

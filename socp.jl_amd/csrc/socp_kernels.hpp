@@ -28,6 +28,9 @@ const SmallVariant* small_variants(int* count);
 // socp_large.hip: one 512-thread workgroup per problem, the problem's vectors
 // in LDS, its matrices in a per-workgroup slot of an HBM workspace.
 constexpr int LARGE_NB_MAX = 8;  // NPAD, MPAD <= 512: a swept panel row lives in registers
+// NPAD <= 2048 where H is factored (the default, not SOCP_F_EXPLICIT_INVERSE):
+// panels wider than 512 are factored in windows (socp_large.hip panel_chol_wide)
+constexpr int LARGE_NB_MAX_CHOL = 32;
 // k bound of the blocked kernel: its LDS / vector offsets and the row offsets
 // into X (KP x NPAD) are 32-bit ints (socp_api.hip large_fits)
 constexpr int LARGE_KMAX = 1 << 21;

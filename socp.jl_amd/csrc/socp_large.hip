@@ -1320,7 +1320,153 @@ struct Large {
     }
     return true;
   }
+  // CHOL panels wider than panel_tiles' register window (NPAD > 512: more than
+  // 32 tile columns right of the panel's block).  The window of WT tile columns
+  // starting at the P block runs panel_tiles' forward pass (the four tile
+  // factorisations); the tiles each step publishes -- Y_s (s < t) and W_t' --
+  // are also saved to the workspace (Yp: unused while chol runs), and each
+  // later window of WT tile columns replays the four steps with them.  Every
+  // tile gets the operations panel_tiles would apply, in the same order, so the
+  // factor does not depend on the window.  Stores as panel_tiles<CHOL>.
+  static constexpr int WJ = 4, WTC = WJ * NW;  // tile columns per wave / per window
+  __device__ bool panel_chol_wide(gdbl* M, int ld, int P, int NT) {
+    const int w = wv, P0 = 64 * P, ob = L.o_row, of = L.o_rv, J0 = 4 * P;
+    gdbl* const sv = Yp;  // step t's tiles: slot 4t + s (Y_s, s < t), 4t + 3 (W_t'), lane order
+    const d4 zero = {0.0, 0.0, 0.0, 0.0};
+    for (int jw = J0; jw < NT; jw += WTC) {
+      const bool first = jw == J0;
+      d4 R[4][WJ];
+      {
+        LANE_IDS();
+#pragma unroll
+        for (int i = 0; i < WJ; ++i) {
+          const int j = jw + w + NW * i;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int x = P0 + 16 * t + g + 4 * r, y = 16 * j + cl;  // element (x, y), lower triangle
+              R[t][i][r] = j < NT ? M[(y <= x) ? (int64_t)y * ld + x : (int64_t)x * ld + y] : 0.0;
+            }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        LANE_IDS();
+        const int jd = J0 + t;  // in the first window: wave t, register column 0
+        d4 Yb[4], WTt;
+        if (first) {
+          if (w == t) {
+            d4 C = R[t][0], Ys[4];
+#pragma unroll
+            for (int s_ = 0; s_ < t; ++s_) Ys[s_] = R[s_][0];
+#pragma unroll
+            for (int s_ = 0; s_ < t; ++s_) C = tile_mm<1>(Ys[s_], Ys[s_], C);  // D_tt - sum L_ts L_ts'
+            d4 Wt;
+            bool ok = true;
+            factor_tile<SOCP_LG_TILE_INPLACE != 0>(C, Wt, ok);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+              for (int s_ = 0; s_ < t; ++s_) LV(ob + 256 * s_ + 64 * r + lane) = Ys[s_][r];
+              LV(ob + 768 + 64 * r + lane) = Wt[r];
+            }
+            if (lane == 0) LV(of + t) = ok ? 0.0 : 1.0;
+            R[t][0] = Wt;  // E's diagonal tile
+          }
+          LDS_BAR();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+#pragma unroll
+            for (int s_ = 0; s_ < t; ++s_) Yb[s_][r] = LV(ob + 256 * s_ + 64 * r + lane);
+            WTt[r] = LV(ob + 768 + 64 * (cl >> 2) + 16 * (cl & 3) + g + 4 * r);  // W_t'
+          }
+          if (w == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+              for (int s_ = 0; s_ < t; ++s_) sv[(4 * t + s_) * 256 + 64 * r + lane] = Yb[s_][r];
+              sv[(4 * t + 3) * 256 + 64 * r + lane] = WTt[r];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+#pragma unroll
+            for (int s_ = 0; s_ < t; ++s_) Yb[s_][r] = sv[(4 * t + s_) * 256 + 64 * r + lane];
+            WTt[r] = sv[(4 * t + 3) * 256 + 64 * r + lane];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < WJ; ++i) {
+          const int j = jw + w + NW * i;
+          if (j >= NT || j == jd) continue;
+          const int u = ((j >> 2) == P) ? (j & 3) : -1;  // P-block tile column index
+          d4 X = (u >= 0 && u < t) ? zero : R[t][i];      // E: the identity's zero below
+#pragma unroll
+          for (int s_ = 0; s_ < t; ++s_)
+            if (u < 0 || u >= t || s_ >= u) X = tile_mm<1>(Yb[s_], R[s_][i], X);
+          R[t][i] = tile_mm<0>(WTt, X, zero);
+        }
+        if (first) LDS_BAR();  // the slots are rewritten by the next step
+      }
+      if (first) {
+        bool ok = true;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) ok = ok && LV(of + t) == 0.0;
+        if (!ok) return false;  // uniform: every wave read the same flags
+      }
+      {
+        LANE_IDS();
+#pragma unroll
+        for (int i = 0; i < WJ; ++i) {
+          const int j = jw + w + NW * i;
+          if (j >= NT) continue;
+          const bool pb = (j >> 2) == P;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int x = P0 + 16 * t + g + 4 * r, y = 16 * j + cl;  // tile element (x, y)
+              if (!pb)
+                M[(int64_t)x * ld + y] = R[t][i][r];  // L[y][x]: column x of L, coalesced
+              else if ((j & 3) <= t && y <= x)
+                M[(int64_t)y * ld + x] = R[t][i][r];  // E[x][y]
+            }
+        }
+      }
+      if (first) BAR();  // the saved step tiles visible to every wave
+    }
+    if (tid < 64) Rv[P0 + tid] = -1.0;
+    return true;
+  }
+  // chol_nb with a runtime panel count and panel_chol_wide (NPAD > 512)
+  __device__ bool chol_wide(gdbl* M, int ld) {
+    const int nb = ld / 64;
+    for (int P = 0; P < nb; ++P) {
+      if (P > 0) {
+        for (int t = P + wv; t < nb; t += NW) {
+          d4 acc[4][4];
+          if (t == P) {
+            load_blkT<true>(acc, M, ld, 64 * t, 64 * P);
+            for (int Q = 0; Q < P; ++Q) gram_blkT<true>(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q);
+            store_blkT<true>(acc, M, ld, 64 * t, 64 * P);
+          } else {
+            load_blkT(acc, M, ld, 64 * t, 64 * P);
+            for (int Q = 0; Q < P; ++Q) gram_blkT(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q);
+            store_blkT(acc, M, ld, 64 * t, 64 * P);
+          }
+        }
+        BAR();
+      }
+      const bool ok = panel_chol_wide(M, ld, P, 4 * nb);
+      if (!ok) return false;
+      BAR();  // L's panel P complete before the next catch-up reads it
+    }
+    return true;
+  }
   __device__ bool chol(gdbl* M, int ld) {
+    if (ld > 64 * LARGE_NB_MAX) return chol_wide(M, ld);
     switch (ld / 64) {
       case 1: return chol_nb<1>(M, ld);
       case 2: return chol_nb<2>(M, ld);

@@ -611,6 +611,9 @@ __device__ __forceinline__ double rsqrt_tile(double d) {
 #ifndef SOCP_TRANSPOSE_MFMA
 #define SOCP_TRANSPOSE_MFMA 0
 #endif
+#ifndef SOCP_U_LANECONES
+#define SOCP_U_LANECONES 0  // 1: compute_U takes the cone descriptors from the cone lanes
+#endif
 #ifndef SOCP_TILE_OKDIAG
 #define SOCP_TILE_OKDIAG 0  // 1: the pivot test once per tile, on the diagonal of W
 #endif
@@ -820,6 +823,7 @@ struct Small {
       if constexpr (HOIST_CST) {
         lc_soc = a.cones.kind[lane] == SOC_K;
         lc_off = a.cones.offs[lane];
+        lc_dim = a.cones.dim[lane];
       }
     }
     for (int i = lane; i < KP; i += 64) {
@@ -869,7 +873,7 @@ struct Small {
   // lane c < nc: its cone's kind and offset (per-cone work without the table
   // round trips)
   bool lc_soc = false;
-  int lc_off = 0;
+  int lc_off = 0, lc_dim = 0;
   __device__ __forceinline__ void load_problem(int64_t p) {
     MARK_BEGIN("load_problem");
     LANE_IDS();
@@ -1589,11 +1593,32 @@ struct Small {
 #pragma unroll
       for (int pp = 0; pp < NP; ++pp) wall[pp] = LDS(WB + 4 * pp + g);
     }
+#if SOCP_U_LANECONES
+    // every SOC cone's offset, dim, head weight and 1/(1+wb0) on its cone lane
+    // (lane c < nc), read in one round trip with the row weights; the loop
+    // takes them by readlane (no scalar-memory or LDS wait per cone)
+    bool socl = false;
+    int ol = 0, dl = 0;
+    double hwl = 0.0, invl = 0.0;
+    if (lane < nc) {
+      socl = HOIST_CST ? lc_soc : (int)LDS(O_CKIND + lane) == SOC_K;
+      ol = HOIST_CST ? lc_off : (int)LDS(O_COFF + lane);
+      dl = HOIST_CST ? lc_dim : (int)LDS(O_CDIM + lane);
+      hwl = -(1.0 + LDS(WB + ol));
+      invl = LDS(cc(CC_I1, lane));
+    }
+    for (uint64_t mk = __ballot(socl); mk; mk &= mk - 1) {
+      const int c = __builtin_ctzll(mk);
+      const int o = __builtin_amdgcn_readlane(ol, c), d = __builtin_amdgcn_readlane(dl, c);
+      const double hw = readlane_d(hwl, c);  // the head row's weight
+      const double inv = readlane_d(invl, c);
+#else
     for (int c = 0; c < nc; ++c) {
       if (a.cones.kind[c] != SOC_K) continue;
       const int o = a.cones.offs[c], d = a.cones.dim[c];
       const double hw = -(1.0 + LDS(WB + o));  // the head row's weight
       const double inv = LDS(cc(CC_I1, c));
+#endif
       const int p0 = o >> 2, p1 = (o + d + 3) >> 2;  // row steps [p0, p1) meet the cone
       double acc[NQ];
 #pragma unroll

@@ -46,9 +46,12 @@ def test_supported_dims():
         cfg = CONFIGS[name]
         d = _lib.Dims(cfg.batch, cfg.n, cfg.m, cfg.k, len(cfg.cones))
         assert bool(L.socp_supported(C.byref(d))) == ok, name
-    # beyond the blocked kernel: n > 512, m > 512, or more than 64 cones
-    for n, m, k, nc in ((600, 0, 601, 1), (64, 600, 128, 1), (256, 0, 130, 65)):
+    # beyond the blocked kernel: n > 2048, m > 512, or more than 64 cones
+    for n, m, k, nc in ((2049, 0, 2050, 1), (64, 600, 128, 1), (256, 0, 130, 65)):
         assert not L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
+    # n > 512: the blocked kernel's windowed wide panels (Cholesky order)
+    for n, m, k, nc in ((600, 0, 601, 1), (2048, 512, 2100, 8)):
+        assert L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
     # k-vectors over the 160 KiB LDS run with the vectors in HBM (the GV kernels)
     for n, m, k, nc in ((512, 64, 1000, 8), (64, 16, 4096, 4), (64, 16, 1 << 21, 4)):
         assert L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)

@@ -170,6 +170,45 @@ def test_wide_k_global_vector_kernel(oracle):
     assert_trajectory(cfg, g, r, B, 1e-8, "xi")
 
 
+WIDE_N = [
+    # the verdict's shape: one SOC(601), m = 0 (NPAD 640: the first window and one more)
+    dict(n=600, m=0, k=601, cones=[(1, 0, 601)], seed=0x534F4350 + 12, B=2, K=(1, 2)),
+    # POC + SOC, m > 0, an odd block count (NPAD 704)
+    dict(n=700, m=40, k=800, cones=[(0, 0, 160)] + [(1, 160 * i, 160) for i in range(1, 5)],
+         seed=0x534F4350 + 13, B=2, K=(1, 2)),
+    # three windows per early panel, vectors beyond the LDS (the GV kernel)
+    # (the reference order's dense k^3 iW*iW' takes the oracle ~20 s here: kernel order only)
+    dict(n=1100, m=64, k=1200, cones=[(1, 150 * i, 150) for i in range(8)], seed=0x534F4350 + 14, B=1, K=(1,),
+         ref=False),
+]
+
+
+@pytest.mark.parametrize("shape", WIDE_N, ids=lambda s: f"n{s['n']}")
+def test_wide_n_blocked_cholesky(oracle, shape):
+    """n > 512 (densesolver.jl:19-38 allocates for any n): the blocked kernel
+    factors H = L L' by 64-column panels whose right-hand part (more than 32
+    tile columns) is transformed in windows that replay the panel's four tile
+    steps (panel_chol_wide).  Iterates vs the oracle in the kernel's operation
+    order (X = W^-1 G, Cholesky + triangular solves) rel <= 1e-8, and vs the
+    reference's own order at the first iteration; the explicit-inverse order
+    (a swept panel row in registers) stays limited to n <= 512."""
+    from types import SimpleNamespace
+    cfg = SimpleNamespace(**shape)
+    B = shape["B"]
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    for K in shape["K"]:
+        r = oracle_run(oracle, cfg, d, params=oracle.Params(maxit=K, tol=0.0,
+                                                            flags=oracle.F_STRUCTURED | oracle.F_CHOLSOLVE))
+        g = run(cfg, d, maxit=K, tol=0.0)
+        assert S.default_context().last_kernel_name().startswith("socp_large")
+        assert (g["status"] == S.MAXIT).all(), g["status"]
+        assert_trajectory(cfg, g, r, B, 1e-8, K)
+    if shape.get("ref", True):
+        r = oracle_run(oracle, cfg, d, params=oracle.Params(maxit=1, tol=0.0))
+        g = run(cfg, d, maxit=1, tol=0.0)
+        assert_trajectory(cfg, g, r, B, 1e-8, "reference order")
+
+
 def test_c4_trajectory_k1_to_k5_fixture():
     """C4 at its bench K: the 4 committed oracle trajectories (tests/golden/
     trajectories.json, cases C4#0..3) solved as one batch for K = 1..5.  kappa_2(H)

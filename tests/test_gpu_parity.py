@@ -89,12 +89,15 @@ def test_sing_batch_c0b(oracle):
 
 
 def test_beyond_both_kernels_reports_unsupported():
-    # n = 600 > 512: outside the blocked kernel too (the n=150 runtests.jl problem
-    # and C4 run on the blocked kernel: tests/test_gpu_large.py)
-    n, m, k = 600, 0, 601
-    with pytest.raises(S.SocpError) as e:
-        S.batch_solve([(1, 0, k)], n, m, k, np.zeros(n), None, None, np.zeros(k * n), np.zeros(k))
-    assert e.value.code == -2
+    # n > 2048 and, for the explicit-inverse order (a swept panel row in
+    # registers), n > 512: outside the blocked kernel (n = 600 in the default
+    # order solves: tests/test_gpu_large.py::test_wide_n_*)
+    for n, xi in ((2100, False), (600, True)):
+        k = n + 1
+        with pytest.raises(S.SocpError) as e:
+            S.batch_solve([(1, 0, k)], n, 0, k, np.zeros(n), None, None, np.zeros(k * n), np.zeros(k),
+                          explicit_inverse=xi)
+        assert e.value.code == -2, (n, xi)
 
 
 # ------------------------------------------------------------ generator
