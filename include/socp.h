@@ -114,9 +114,10 @@ int socp_ctx_reset_stream(socp_ctx* ctx);
 /* 1 if a compiled kernel accepts the dims: the register-resident kernel (one
  * wavefront per problem, <= 8 cones, m <= 64; k <= 128 for n <= 48, k <= 96
  * for 48 < n <= 64: the compiled variant table, socp.jl_amd/csrc/gen_inst.py)
- * or the blocked kernel (n, m <= 512, <= 64 cones, k <= 2^21 -- its LDS /
- * vector offsets are 32-bit; one 512-thread workgroup per problem), which also
- * takes every register-kernel shape.  The
+ * or the blocked kernel (n, m <= 2048 -- 512 with SOCP_F_EXPLICIT_INVERSE,
+ * whose sweeps hold a panel row in registers --, <= 64 cones, k <= 2^21 -- its
+ * LDS / vector offsets are 32-bit; one 512-thread workgroup per problem), which
+ * also takes every register-kernel shape.  The
  * blocked kernel keeps the problem's vectors in the 160 KiB LDS of a CU when
  * they fit (C4, n=512 m=64 k=640, uses 126 KiB) and in its HBM workspace slot
  * otherwise (e.g. k = 1000 at n = 512).  Other shapes return

@@ -240,10 +240,12 @@ static bool large_fits(int n, int m, int k, int nc, size_t* lds_bytes, bool* gv 
     if (lds_total > INT32_MAX / 2 || KP * RW > INT32_MAX) return false;
   }
   const LargeLayout L = large_layout(n, m, k);
-  // n: up to 64 LARGE_NB_MAX_CHOL with the Cholesky factor (wide panels in
-  // windows, socp_large.hip panel_chol_wide), 64 LARGE_NB_MAX where H is swept
-  // (SOCP_F_EXPLICIT_INVERSE: a panel row in registers); m: S is always swept
-  if (L.NPAD > 64 * (xi ? LARGE_NB_MAX : LARGE_NB_MAX_CHOL) || L.MPAD > 64 * LARGE_NB_MAX || nc > MAXC) return false;
+  // n, m: up to 64 LARGE_NB_MAX_CHOL with Cholesky factors of H and S (wide
+  // panels in windows, socp_large.hip panel_chol_wide; S is swept up to 512),
+  // 64 LARGE_NB_MAX where H and S are swept (SOCP_F_EXPLICIT_INVERSE: a panel
+  // row in registers)
+  const int nb_max = xi ? LARGE_NB_MAX : LARGE_NB_MAX_CHOL;
+  if (L.NPAD > 64 * nb_max || L.MPAD > 64 * nb_max || nc > MAXC) return false;
   size_t lds = (size_t)L.total * sizeof(double);
   const bool g = lds + 64 > 160 * 1024;
   if (g) lds = 64 * sizeof(double);
@@ -260,7 +262,7 @@ extern "C" int socp_supported(const socp_dims* d) {
 
 static const char* kUnsupported =
     "dims outside both kernels (register-resident: n, m <= 64, k <= 128, <= 8 cones; "
-    "blocked: n <= 2048 (512 with SOCP_F_EXPLICIT_INVERSE), m <= 512, <= 64 cones, k <= 2^21)";
+    "blocked: n, m <= 2048 (512 with SOCP_F_EXPLICIT_INVERSE), <= 64 cones, k <= 2^21)";
 
 // ---------------------------------------------------------------- launch
 static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_DIAG builds)
@@ -851,7 +853,7 @@ static void sqr_free(socp_sqr* h) {
 }
 
 static bool sqr_fits(const socp_dims* d, size_t* lds) {
-  if (d->n > SQR_LMAX || d->m > SQR_LMAX || d->k > SQR_KMAX) return false;
+  if (d->n < 0 || d->m < 0 || d->k < 0 || d->n > SQR_LMAX || d->m > SQR_LMAX || d->k > SQR_KMAX) return false;
   const size_t bytes = (size_t)sqr_layout(d->n, d->m, d->k, d->ncones).total * sizeof(double);
   if (lds) *lds = bytes;
   return bytes <= 160 * 1024;
@@ -901,7 +903,7 @@ extern "C" int socp_sqr_create(socp_ctx* ctx, const socp_dims* dims, const int32
   if (rc) return bail(rc);
   h->deg = degree;
   if (!sqr_fits(dims, &h->lds))
-    return bail(fail(SOCP_E_UNSUPPORTED, "rank-update plugin: n, m <= 160, k <= 256, LDS layout <= 160 KiB (socp_sqr.hip)"));
+    return bail(fail(SOCP_E_UNSUPPORTED, "rank-update plugin: n, m <= 1024, k <= 4096, LDS layout <= 160 KiB (socp_sqr.hip)"));
   const int64_t B = dims->batch;
   const int n = dims->n, m = dims->m, k = dims->k;
   if (B > 0 && (!G || (m > 0 && !A))) return bail(fail(SOCP_E_INVALID, "NULL data pointer"));
@@ -1048,6 +1050,8 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
   socp_params P;
   if (params) P = *params; else socp_params_default(&P);
   if (P.maxit < 0) return fail(SOCP_E_INVALID, "maxit < 0");
+  if (sqr_ipm_lds_bytes(n, m, k) > 160 * 1024)
+    return fail(SOCP_E_UNSUPPORTED, "socp_sqr_solve_socp: the IPM kernels' vectors (7 k + n + m doubles) exceed 160 KiB");
   socp_ctx* ctx = h->ctx;
   HIPCHK(hipSetDevice(ctx->device));
   h->h2d_bytes = 0;

@@ -1812,6 +1812,14 @@ struct Large {
     BAR();
     LSTAMP(SP_SCHUR);
     }
+    if (CHOL && L.MPAD > 64 * LARGE_NB_MAX) {
+      // m > 512: S = L_S L_S' in place (the windowed panels of chol_wide); the
+      // solves apply S^-1 as two triangular solves.  cholesky! of S fails
+      // where this does (densesolver.jl:51)
+      if (!chol(Sm, L.MPAD)) return ST_CHOL_S;
+      LSTAMP(SP_SCHUR);
+      return 0;
+    }
     if (!sweep(Sm, L.MPAD)) return ST_CHOL_S;
     finalize_sym(Sm, L.MPAD);
     LSTAMP(SP_SCHUR);
@@ -2032,8 +2040,9 @@ struct Large {
   // (padding) are never read.
   // out = L^-1 in: r = in_P - L_P,<P out_<P (lanes = rows, wavefronts split
   // the columns; partial sums through LDS), out_P = E_P r.
-  __device__ void trsv_fwd(gcdbl* Lm, int ld, int vin, int vout) {
-    const int NB = L.NPAD / 64, p1 = L.o_part, p2 = L.o_fx;
+  // (dim: the factor's order -- n for H, m for S; ld = its padded order)
+  __device__ void trsv_fwd(gcdbl* Lm, int ld, int vin, int vout, int dim) {
+    const int NB = ld / 64, p1 = L.o_part, p2 = L.o_fx, n = dim;
     LSTAMP(SP_SOLVE);
     for (int P = 0; P < NB; ++P) {
       const int P0 = 64 * P, i = P0 + lane;
@@ -2066,8 +2075,8 @@ struct Large {
   // out = L^-T in, last block first: r = in_P - L_>P,P' out_>P, out_P = E_P' r.
   // Both products read columns of L / E (contiguous): 16 lanes per column,
   // four columns per wavefront step.
-  __device__ void trsv_bwd(gcdbl* Lm, int ld, int vin, int vout) {
-    const int NB = L.NPAD / 64, p1 = L.o_part, q = lane >> 4, c = lane & 15;
+  __device__ void trsv_bwd(gcdbl* Lm, int ld, int vin, int vout, int dim) {
+    const int NB = ld / 64, p1 = L.o_part, q = lane >> 4, c = lane & 15, n = dim;
     LSTAMP(SP_SOLVE);
     for (int P = NB - 1; P >= 0; --P) {
       const int P0 = 64 * P;
@@ -2138,13 +2147,18 @@ struct Large {
     if constexpr (CHOL) {
     // Li = L^-T L^-1: u = L^-1 n0; m0 = A Li n0 - dy = Z'u - dy; cy = S^-1 m0;
     // cx = Li (n0 + A'm0) = L^-T (u + Z m0)
-    trsv_fwd(Hm, L.NPAD, N0, TN);
+    trsv_fwd(Hm, L.NPAD, N0, TN, n);
     mat_mv(Tm, TN, RP, M0);
-    symv(Sm, L.MPAD, M0, RY);
+    if (L.MPAD > 64 * LARGE_NB_MAX) {  // S = L_S L_S' (factor() factors S beyond the sweep's reach)
+      trsv_fwd(Sm, L.MPAD, M0, M0, m);
+      trsv_bwd(Sm, L.MPAD, M0, RY, m);
+    } else {
+      symv(Sm, L.MPAD, M0, RY);
+    }
     for (int r = tid; r < m; r += NTH) LV(M0 + r) = (sing && !init) ? LV(RP + r) - LV(RY + r) : -LV(RY + r);
     BAR();
     z_mv_add(TN, M0, N0);
-    trsv_bwd(Hm, L.NPAD, N0, RX);
+    trsv_bwd(Hm, L.NPAD, N0, RX, n);
     } else {
     symv(Hm, L.NPAD, N0, TN);
     A_mv(TN, RP, M0);

@@ -91,6 +91,9 @@ enum : int {
   O_FIXED = O_STAMPS + SOCP_NSTAMP_SLOTS  // then (Shape): rcode[KP], 17 k-vectors KS apart, ...
 };
 constexpr int NKV = 17;
+#ifndef SOCP_SYRK_UBT
+#define SOCP_SYRK_UBT 0  // 1: the SYRK's U-row addresses from a launch-wide table
+#endif
 // per-cone constants (SOC cones), recomputed by every scaling:
 //   MU = mu, IMU = 1/mu, WB0 = wbar_0, I1 = 1/(1+wbar_0), W2 = |wbar_1|^2,
 //   L0 = lambda_0, AA = lambda_0^2 - |lambda_1|^2 (iprod!'s `a`, vectors.jl:105),
@@ -144,7 +147,11 @@ struct Shape {
   // (AL_LDS) in the k-vectors dead during a factorisation when they hold it
   static constexpr bool TB_ALIAS = AL_LDS && NKV_DEAD * KS >= 16 * 17;
   static constexpr int O_TB = TB_ALIAS ? O_KV + KV_RZ * KS : O_U + UAL;
-  static constexpr int TOTAL = O_U + UAL + (TB_ALIAS ? 0 : 16 * 17);
+  // the SYRK's U-row table (int32 per k-row) where the LDS allows (not the
+  // two-wave shapes, whose LDS is tight)
+  static constexpr bool UBT = SOCP_SYRK_UBT && NQ * NP > 24 && NQ > 1;
+  static constexpr int O_UBT = O_U + UAL + (TB_ALIAS ? 0 : 16 * 17);
+  static constexpr int TOTAL = O_UBT + (UBT ? (KP + 1) / 2 : 0);
   static constexpr int nv(int id) { return O_NV + id * NPAD; }
   static constexpr int mv(int id) { return O_MV + id * MPAD; }
 };
@@ -164,7 +171,9 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
   int KS = 4 * NP;  // Shape::KS
   int ual = (MQ == 1 && MPAD * LDA > NCS * NPAD) ? MPAD * LDA : NCS * NPAD;  // Shape::UAL
   const bool tb_alias = MQ == 1 && NKV_DEAD * KS >= 16 * 17;                // Shape::TB_ALIAS
-  int total = O_FIXED + KS + NKV * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + ual + (tb_alias ? 0 : 16 * 17);
+  const bool ubt = SOCP_SYRK_UBT && NQ * NP > 24 && NQ > 1;                   // Shape::UBT
+  int total = O_FIXED + KS + NKV * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + ual + (tb_alias ? 0 : 16 * 17) +
+              (ubt ? (KS + 1) / 2 : 0);
   return (size_t)total * sizeof(double);
 }
 
@@ -612,10 +621,10 @@ __device__ __forceinline__ double rsqrt_tile(double d) {
 #define SOCP_TRANSPOSE_MFMA 0
 #endif
 #ifndef SOCP_U_LANECONES
-#define SOCP_U_LANECONES 0  // 1: compute_U takes the cone descriptors from the cone lanes
+#define SOCP_U_LANECONES 1  // compute_U takes the cone descriptors from the cone lanes (0: from the kernel args)
 #endif
 #ifndef SOCP_TILE_OKDIAG
-#define SOCP_TILE_OKDIAG 0  // 1: the pivot test once per tile, on the diagonal of W
+#define SOCP_TILE_OKDIAG 1  // the pivot test once per tile, on the diagonal of W (0: per pivot)
 #endif
 #ifndef SOCP_TILE_INPLACE
 #define SOCP_TILE_INPLACE 1  // 0: copy back only registers > B (A/B builds)
@@ -815,6 +824,9 @@ struct Small {
         n(args.n), m(args.m), k(args.k), nc(args.nc) {}
 
   // ---------------------------------------------------------------- setup
+  // O_U + cone(row) * NPAD per k-row (int32, launch-wide: the cone table is
+  // the batch's), for the SYRK's U rows (SOCP_SYRK_UBT shapes)
+  __device__ __forceinline__ int ubt(int row) const { return reinterpret_cast<const int*>(socp_lds + SH::O_UBT)[row]; }
   __device__ __forceinline__ void init_tables() {
     if (lane < nc) {
       LDS(O_COFF + lane) = a.cones.offs[lane];
@@ -838,6 +850,7 @@ struct Small {
         }
       }
       LDS(O_RC + i) = (double)code;
+      if constexpr (SH::UBT) reinterpret_cast<int*>(socp_lds + SH::O_UBT)[i] = O_U + (code >> 2) * NPAD;
     }
     // segment partials: entry (v, c, slot) is written only when cone c meets the
     // slot, the same for every problem of the launch; the rest stays zero
@@ -867,7 +880,10 @@ struct Small {
 
 #ifndef SOCP_KO
 #define SOCP_KO 0  // timing knock-outs (tuning builds only; results are wrong): 1 G loaded once per wave,
-                   // 2 no residuals, 4 no compute_U, 8 no S factorisation
+                   // 2 no residuals, 4 no compute_U, 8 no S factorisation, 16 no Gx, 32 no G'z (residuals),
+                   // 128 no A products (residuals), 256 no triangular solves, 512 / 1024 no G products
+                   // in the solves, 2048 no S solves, 4096 no scaling, 8192 no solve head,
+                   // 16384 no solve tail, 32768 no corrector, 65536 no SYRK (H = I), 131072 no chol
 #endif
   bool ko_gloaded = false;
   // lane c < nc: its cone's kind and offset (per-cone work without the table
@@ -1153,6 +1169,11 @@ struct Small {
   // per element.
   __device__ __forceinline__ bool scaling_op(double& ll, bool& dm_aa, bool write_ds) {
     MARK_BEGIN("scaling_op");
+    if (SOCP_KO & 4096) {
+      ll = 1.0;
+      dm_aa = false;
+      return false;
+    }
     LANE_IDS();
     double v[2][3], zi[2], si[2];
 #pragma unroll
@@ -1279,6 +1300,7 @@ struct Small {
   // reciprocal kept in IL.  In: DS, DZ.  Out: K0, K2, T2, DLT (per cone).
   __device__ __forceinline__ void solve_head() {
     MARK_BEGIN("solve_head");
+    if (SOCP_KO & 8192) return;
     LANE_IDS();
     double v[2][3], x[2], x0[2], dz[2], dz0[2], lam[2], wb[2];
 #pragma unroll
@@ -1374,6 +1396,10 @@ struct Small {
   // length (dom: DomainError).
   __device__ __forceinline__ double solve_tail(bool do_step, bool dm_aa, int& dom) {
     MARK_BEGIN("solve_tail");
+    if (SOCP_KO & 16384) {
+      dom = 0;
+      return 1.0;
+    }
     LANE_IDS();
     double v[2][3], k1[2], k10[2], k0[2], k00[2], wb[2], lam[2];
 #pragma unroll
@@ -1493,6 +1519,7 @@ struct Small {
   // In: K0 (kt2), T1 (kt3), KK, DS, DZ, RD, RP.
   __device__ __forceinline__ void affine_post(double tstep, double ll) {
     MARK_BEGIN("affine_post");
+    if (SOCP_KO & 32768) return;
     LANE_IDS();
     double kk = 0.0, kv[NCS];  // one round trip
 #pragma unroll
@@ -1685,7 +1712,18 @@ struct Small {
     double ca, cb;
     int ub;  // LDS index of the cone's U row + cl
   };
-  __device__ __forceinline__ XCoef genX_a(int pp) {
+#if SOCP_SYRK_UBT
+  // (the lane ids of form_H, computed once for the whole product)
+  __device__ __forceinline__ XCoef genX_a(int pp, int g, int cl) {
+    const int row = 4 * pp + g;
+    XCoef c;
+    c.ca = LDS(CA + row);
+    c.cb = LDS(CBV + row);
+    c.ub = ubt(row) + cl;  // O_U + cone(row) * NPAD, from the launch's table
+    return c;
+  }
+#else
+  __device__ __forceinline__ XCoef genX_a(int pp, int, int) {
     LANE_IDS();
     const int row = 4 * pp + g;
     XCoef c;
@@ -1694,6 +1732,7 @@ struct Small {
     c.ub = O_U + (((int)LDS(O_RC + row)) >> 2) * NPAD + cl;
     return c;
   }
+#endif
   __device__ __forceinline__ void genX_b(int pp, const XCoef& c, double (&X)[NQ]) {
     double u[NQ];
 #pragma unroll
@@ -1705,23 +1744,35 @@ struct Small {
       for (int q = 0; q < NQ; ++q) X[q] = fma(c.ca, gr[q], c.cb * u[q]);
     }
   }
+  static constexpr bool diag_tile(int t) {
+    for (int i = 0; i < NQ; ++i)
+      if (tri(i, i) == t) return true;
+    return false;
+  }
   __device__ __forceinline__ void form_H(bool addAA) {
     MARK_BEGIN("form_H");
     LANE_IDS();
+    if (SOCP_KO & 65536) {  // H = I
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) T[t][r] = (diag_tile(t) && g + 4 * r == cl) ? 1.0 : 0.0;
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) T[t] = (d4){0.0, 0.0, 0.0, 0.0};
 #if SOCP_SYRK_PIPE == 2
     double Xc[NQ];
     XCoef c1;
     {
-      const XCoef c0 = genX_a(0);
-      if (NP > 1) c1 = genX_a(1 < NP ? 1 : 0);
+      const XCoef c0 = genX_a(0, g, cl);
+      if (NP > 1) c1 = genX_a(1 < NP ? 1 : 0, g, cl);
       genX_b(0, c0, Xc);
     }
 #pragma unroll
     for (int pp = 0; pp < NP; ++pp) {
       XCoef c2 = c1;
-      if (pp + 2 < NP) c2 = genX_a(pp + 2 < NP ? pp + 2 : 0);
+      if (pp + 2 < NP) c2 = genX_a(pp + 2 < NP ? pp + 2 : 0, g, cl);
       double Xn[NQ];
       if (pp + 1 < NP) genX_b(pp + 1 < NP ? pp + 1 : 0, c1, Xn);
 #pragma unroll
@@ -2066,6 +2117,12 @@ struct Small {
     }
   }
   __device__ __forceinline__ bool chol() {
+    if (SOCP_KO & 131072) {
+      LANE_IDS();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Sv[0][r] = (g + 4 * r == cl) ? 1.0 : 0.0;
+      return true;
+    }
     Sv[0] = (d4){0.0, 0.0, 0.0, 0.0};
     bool ok = true;
     d4 W;

@@ -860,7 +860,7 @@ __device__ __forceinline__ void setup_problem_wg(Ctx& C, int64_t p, int tid) {
   const bool sing = a.sing && a.sing[p];
   double* rec = a.rec + p * L.rec;
   if (a.active && !a.active[p]) return;  // uniform over the workgroup
-  double* P = lds + L.o_L;
+  double* P = L.gfac ? rec + L.r_P : lds + L.o_L;  // the packed factor of H
   double* rdg = lds + L.o_nv;  // 1 / diag of the current factor
   for (int i = tid; i < k; i += SQR_LT) {
     lds[L.o_s + i] = a.s[p * k + i];
@@ -957,10 +957,10 @@ __device__ __forceinline__ void setup_problem_wg(Ctx& C, int64_t p, int tid) {
     bar();
     if (m > 0) {
       // C = L^-1 A' (spsolver.jl:80-82), SQR_RC right-hand sides at a time
-      double* Cc = lds + L.o_C;  // Cc[t * n + i]
       double* Cg = rec + L.r_C;   // C[q * n + i]
       for (int q0 = 0; q0 < m; q0 += SQR_RC) {
         const int nr = (m - q0) < SQR_RC ? (m - q0) : SQR_RC;
+        double* Cc = L.gfac ? Cg + (int64_t)q0 * n : lds + L.o_C;  // Cc[t * n + i]
         bar();
         for (int e = tid; e < nr * n; e += SQR_LT) {
           const int t = e / n, i = e % n;
@@ -977,18 +977,21 @@ __device__ __forceinline__ void setup_problem_wg(Ctx& C, int64_t p, int tid) {
           }
         }
         bar();
-        for (int e = tid; e < nr * n; e += SQR_LT) Cg[(int64_t)q0 * n + e] = Cc[e];
+        if (!L.gfac)
+          for (int e = tid; e < nr * n; e += SQR_LT) Cg[(int64_t)q0 * n + e] = Cc[e];
       }
       __threadfence_block();
       bar();
-      // S = C'C (:83) into the packed triangle (L_H is in the record now), chol(S)
-      syrk_tiles(Cg, n, n, nullptr, nullptr, nullptr, 0, 0, m, P, tid);
+      // S = C'C (:83) into the packed triangle (L_H is in the record now; with
+      // gfac, S's own region: the solves read L_H packed), chol(S)
+      double* PS = L.gfac ? rec + L.r_PS : P;
+      syrk_tiles(Cg, n, n, nullptr, nullptr, nullptr, 0, 0, m, PS, tid);
       double* rds = lds + L.o_rdgs;
-      if (!chol_packed(P, m, rds, tid)) status = SQR_CHOL_S;
+      if (!chol_packed(PS, m, rds, tid)) status = SQR_CHOL_S;
       if (status == 0)
         for (int e = tid; e < m * m; e += SQR_LT) {
           const int i = e % m, j = e / m;
-          rec[L.r_S + e] = i >= j ? P[sqr_pk(i, j, m)] : 0.0;
+          rec[L.r_S + e] = i >= j ? PS[sqr_pk(i, j, m)] : 0.0;
         }
     }
   }
@@ -1031,7 +1034,7 @@ __device__ __forceinline__ void solve_problem_wg(Ctx& C, int64_t p, int tid) {
   double *dz = lds + L.o_s, *ds = lds + L.o_z;
   double *k0 = lds + L.o_D, *k1 = lds + L.o_iW, *k2 = lds + L.o_u, *kt = lds + L.o_v;
   double *n0 = lds + L.o_n0, *nb = lds + L.o_n1, *mv = lds + L.o_mv, *rdg = lds + L.o_nv;
-  double* P = lds + L.o_L;
+  const double* P = L.gfac ? rec + L.r_P : lds + L.o_L;  // the packed factor of H
   for (int i = tid; i < k; i += SQR_LT) {
     lam[i] = rec[L.r_l + i];
     wb[i] = rec[L.r_wb + i];
@@ -1039,10 +1042,11 @@ __device__ __forceinline__ void solve_problem_wg(Ctx& C, int64_t p, int tid) {
     ds[i] = a.ds[p * k + i];
   }
   for (int c = tid; c < nc; c += SQR_LT) mu[c] = rec[L.r_mu + c];
-  for (int e = tid; e < n * n; e += SQR_LT) {
-    const int i = e % n, j = e / n;
-    if (i >= j) P[sqr_pk(i, j, n)] = rec[L.r_L + e];
-  }
+  if (!L.gfac)  // (with gfac the setup left it packed in the record)
+    for (int e = tid; e < n * n; e += SQR_LT) {
+      const int i = e % n, j = e / n;
+      if (i >= j) lds[L.o_L + sqr_pk(i, j, n)] = rec[L.r_L + e];
+    }
   for (int j = tid; j < n; j += SQR_LT) rdg[j] = 1.0 / rec[L.r_L + (int64_t)j * n + j];
   bar();
   // k0 = lam \\ ds; k1 = W k0; k2 = dz - k1; k1 = W^-1 W^-1 k2   (spsolver.jl:90-96)

@@ -8,8 +8,9 @@
 namespace socp {
 
 constexpr int SQR_NMAX = 64;   // n, m <= 64: one row per lane in the triangular solves (wavefront kernels)
-constexpr int SQR_LMAX = 160;  // n, m <= 160: the workgroup kernels (factors packed in LDS)
-constexpr int SQR_KMAX = 256;  // k
+constexpr int SQR_LMAX = 1024;  // n, m <= 1024: the workgroup kernels (factors packed in LDS, or in the
+                                // record where they exceed it: SqrLayout::gfac)
+constexpr int SQR_KMAX = 4096;  // k (and the vectors' LDS footprint <= 160 KiB)
 constexpr int SQR_KC = 8;      // G rows per LDS chunk in the H product
 constexpr int SQR_NW = 66;     // LDS row stride of a chunk (doubles; 16-byte aligned rows)
 constexpr int SQR_RHS = 8;     // right-hand sides per forward sweep in L^-1 A'
@@ -19,6 +20,7 @@ constexpr int SQR_CHOL_H = 2, SQR_CHOL_S = 3, SQR_DOMAIN = 4;  // include/socp.h
 
 struct SqrLayout {
   int large;     // 1: the workgroup kernels (n or m > SQR_NMAX)
+  int gfac;      // 1 (large only): the packed factors and the C chunk in the record, not in LDS
   int ldl, ldm;  // LDS leading dimensions of C = L^-1 A' and L_S (odd: conflict-free row walks)
   // LDS offsets (doubles)
   int o_s, o_z, o_D, o_iW, o_u, o_v, o_l, o_wb, o_one, o_mu, o_rdgs, o_nv, o_mv, o_flag, o_X, o_S, total;
@@ -27,8 +29,9 @@ struct SqrLayout {
   int o_w, o_wv, o_n0, o_n1, o_C, o_L;
   // per-problem factor record (doubles): L_H (n x n, column-major, zeros above
   // the diagonal), L_S (m x m), lambda, wb (k each), mu (nc), status; the
-  // workgroup kernels add C = L^-1 A' (n x m, column-major) as scratch
-  int64_t r_L, r_S, r_l, r_wb, r_mu, r_st, r_C, rec;
+  // workgroup kernels add C = L^-1 A' (n x m, column-major) as scratch, and
+  // with gfac the packed factors of H and S (r_P, r_PS) that LDS holds otherwise
+  int64_t r_L, r_S, r_l, r_wb, r_mu, r_st, r_C, r_P, r_PS, rec;
 };
 
 // packed column-major lower triangle of an N x N matrix: element (i, j), i >= j
@@ -58,6 +61,7 @@ __host__ __device__ inline SqrLayout sqr_layout(int n, int m, int k, int nc) {
   L.o_mv = o;   o += MV;
   L.o_flag = o; o += 2;
   L.o_w = L.o_wv = L.o_n0 = L.o_n1 = L.o_C = L.o_L = 0;
+  L.gfac = 0;
   if (!L.large) {
     L.o_X = o;
     int xs = 2 * SQR_KC * SQR_NW;          // Y row chunks (H product)
@@ -71,9 +75,13 @@ __host__ __device__ inline SqrLayout sqr_layout(int n, int m, int k, int nc) {
     L.o_wv = o; o += NV;
     L.o_n0 = o; o += NV;
     L.o_n1 = o; o += NV;
-    L.o_C = o;  o += ev(n * SQR_RC);
     const int th = n * (n + 1) / 2, ts = m * (m + 1) / 2;
-    L.o_L = o;  o += ev(th > ts ? th : ts);
+    if ((int64_t)(o + ev(n * SQR_RC) + ev(th > ts ? th : ts)) * 8 <= 160 * 1024) {
+      L.o_C = o;  o += ev(n * SQR_RC);
+      L.o_L = o;  o += ev(th > ts ? th : ts);
+    } else {
+      L.gfac = 1;  // packed factors and the C chunk in the record (L1 / L2-cached)
+    }
   }
   L.total = o;
   int64_t r = 0;
@@ -86,6 +94,14 @@ __host__ __device__ inline SqrLayout sqr_layout(int n, int m, int k, int nc) {
   r = (r + 1) / 2 * 2;
   L.r_C = r;
   if (L.large) r += (int64_t)n * m;
+  r = (r + 1) / 2 * 2;
+  L.r_P = L.r_PS = r;
+  if (L.gfac) {
+    r += (int64_t)n * (n + 1) / 2;
+    r = (r + 1) / 2 * 2;
+    L.r_PS = r;
+    r += (int64_t)m * (m + 1) / 2;
+  }
   L.rec = (r + 1) / 2 * 2;
   return L;
 }

@@ -153,7 +153,8 @@ __device__ __forceinline__ double e_of(const ConeTable& C, int i) {
 // its rows' G x and A x running sums, and its share of the column dot
 // products G'z + A'y, which a reduce-scatter over the 16 lanes of a row and a
 // sum over the four rows turn into the 16 columns' totals (lane cl of every
-// row holds column j0 + cl).  k, m <= 256 (SQR_KMAX): four rows per lane.
+// row holds column j0 + cl).  k, m <= 256: four rows per lane (beyond, a
+// two-pass form).
 __device__ void residuals_w(const SqrIpmArgs& a, int64_t p, double* rdv, double* rpv, double* rzv, double (&r3)[3],
                             int lane) {
   const int n = a.n, m = a.m, k = a.k;
@@ -161,6 +162,41 @@ __device__ void residuals_w(const SqrIpmArgs& a, int64_t p, double* rdv, double*
   const double* A = m ? a.A + p * (int64_t)m * n : nullptr;
   const double *x = a.x + p * n, *y = a.y + p * m, *z = a.z + p * k, *s = a.s + p * k;
   const int cl = lane & 15;
+  if (k > 256 || m > 256) {
+    // beyond four rows per lane (the workgroup plugin's large shapes): the
+    // column dot products a column at a time (a wave sum each), then the row
+    // sums a lane per row -- the same sums, summed in another order
+    double d2 = 0.0, p2 = 0.0, zs = 0.0;
+    for (int j = 0; j < n; ++j) {
+      const double* Gj = G + (int64_t)j * k;
+      double pc = 0.0;
+      for (int i = lane; i < k; i += 64) pc = fma(Gj[i], z[i], pc);
+      if (m) {
+        const double* Aj = A + (int64_t)j * m;
+        for (int i = lane; i < m; i += 64) pc = fma(Aj[i], y[i], pc);
+      }
+      const double v = ws64(pc) + a.c[p * n + j];
+      if (lane == 0) rdv[j] = v;
+      d2 += v * v;  // every lane holds v: d2 is the same in all lanes
+    }
+    for (int i = lane; i < k; i += 64) {
+      double gx = 0.0;
+      for (int j = 0; j < n; ++j) gx = fma(G[(int64_t)j * k + i], x[j], gx);
+      if (rzv) rzv[i] = gx + s[i] - a.h[p * k + i];
+      zs += z[i] * s[i];
+    }
+    for (int i = lane; i < m; i += 64) {
+      double ax = 0.0;
+      for (int j = 0; j < n; ++j) ax = fma(A[(int64_t)j * m + i], x[j], ax);
+      const double v = ax - a.b[p * m + i];
+      rpv[i] = v;
+      p2 += v * v;
+    }
+    r3[0] = sqrt(d2);
+    r3[1] = sqrt(ws64(p2));
+    r3[2] = ws64(zs);
+    return;
+  }
   constexpr int R = 4;
   double zr[R], yr[R], gx[R], ax[R];
 #pragma unroll

@@ -46,11 +46,11 @@ def test_supported_dims():
         cfg = CONFIGS[name]
         d = _lib.Dims(cfg.batch, cfg.n, cfg.m, cfg.k, len(cfg.cones))
         assert bool(L.socp_supported(C.byref(d))) == ok, name
-    # beyond the blocked kernel: n > 2048, m > 512, or more than 64 cones
-    for n, m, k, nc in ((2049, 0, 2050, 1), (64, 600, 128, 1), (256, 0, 130, 65)):
+    # beyond the blocked kernel: n or m > 2048, or more than 64 cones
+    for n, m, k, nc in ((2049, 0, 2050, 1), (64, 2100, 128, 1), (256, 0, 130, 65)):
         assert not L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
-    # n > 512: the blocked kernel's windowed wide panels (Cholesky order)
-    for n, m, k, nc in ((600, 0, 601, 1), (2048, 512, 2100, 8)):
+    # n, m > 512: the blocked kernel's windowed wide panels (Cholesky order)
+    for n, m, k, nc in ((600, 0, 601, 1), (2048, 512, 2100, 8), (64, 600, 128, 1), (2048, 2048, 2100, 8)):
         assert L.socp_supported(C.byref(_lib.Dims(1, n, m, k, nc))), (n, m, k)
     # k-vectors over the 160 KiB LDS run with the vectors in HBM (the GV kernels)
     for n, m, k, nc in ((512, 64, 1000, 8), (64, 16, 4096, 4), (64, 16, 1 << 21, 4)):
@@ -124,15 +124,17 @@ def test_host_arrays_are_size_checked():
 
 
 def test_sqr_supported_dims():
-    # the rank-update plugin: n, m <= 160, k <= 256, LDS layout <= 160 KiB (socp_sqr.hpp)
+    # the rank-update plugin: n, m <= 1024, k <= 4096, the vectors' LDS layout
+    # <= 160 KiB (socp_sqr.hpp; factors beyond the LDS live in the record)
     L = _lib.load()
-    for name, ok in (("C0b", True), ("C1", True), ("C2", True), ("C4", False)):
+    for name in ("C0b", "C1", "C2", "C4"):  # C4 (n = 512): the factors in the record
         cfg = CONFIGS[name]
         d = _lib.Dims(cfg.batch, cfg.n, cfg.m, cfg.k, len(cfg.cones))
-        assert bool(L.socp_sqr_supported(C.byref(d))) == ok, name
+        assert L.socp_sqr_supported(C.byref(d)), name
     assert L.socp_sqr_supported(C.byref(_lib.Dims(1, 65, 0, 10, 1)))
     assert L.socp_sqr_supported(C.byref(_lib.Dims(1, 150, 102, 50, 1)))  # runtests.jl:204-244
     assert L.socp_sqr_supported(C.byref(_lib.Dims(1, 160, 160, 256, 16)))
-    assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, 161, 0, 10, 1)))
-    assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, 64, 161, 10, 1)))
-    assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, 64, 0, 257, 1)))
+    for n, m, k in ((161, 0, 10), (64, 161, 10), (64, 0, 257), (400, 100, 500), (1024, 1024, 1100)):
+        assert L.socp_sqr_supported(C.byref(_lib.Dims(1, n, m, k, 1))), (n, m, k)
+    for n, m, k in ((1025, 0, 1100), (64, 1025, 10), (64, 0, 4097), (1024, 1024, 4096)):
+        assert not L.socp_sqr_supported(C.byref(_lib.Dims(1, n, m, k, 1))), (n, m, k)

@@ -177,6 +177,9 @@ WIDE_N = [
     dict(n=700, m=40, k=800, cones=[(0, 0, 160)] + [(1, 160 * i, 160) for i in range(1, 5)],
          seed=0x534F4350 + 13, B=2, K=(1, 2)),
     # three windows per early panel, vectors beyond the LDS (the GV kernel)
+    # m > 512: S = A H^-1 A' by the windowed Cholesky too, applied by two triangular solves
+    dict(n=720, m=600, k=800, cones=[(0, 0, 200)] + [(1, 200 + 150 * i, 150) for i in range(4)],
+         seed=0x534F4350 + 15, B=1, K=(1, 2)),
     # (the reference order's dense k^3 iW*iW' takes the oracle ~20 s here: kernel order only)
     dict(n=1100, m=64, k=1200, cones=[(1, 150 * i, 150) for i in range(8)], seed=0x534F4350 + 14, B=1, K=(1,),
          ref=False),
@@ -185,10 +188,10 @@ WIDE_N = [
 
 @pytest.mark.parametrize("shape", WIDE_N, ids=lambda s: f"n{s['n']}")
 def test_wide_n_blocked_cholesky(oracle, shape):
-    """n > 512 (densesolver.jl:19-38 allocates for any n): the blocked kernel
-    factors H = L L' by 64-column panels whose right-hand part (more than 32
-    tile columns) is transformed in windows that replay the panel's four tile
-    steps (panel_chol_wide).  Iterates vs the oracle in the kernel's operation
+    """n or m > 512 (densesolver.jl:19-38 allocates for any size): the blocked
+    kernel factors H = L L' (and S = A H^-1 A' where m > 512) by 64-column
+    panels whose right-hand part (more than 32 tile columns) is transformed in
+    windows that replay the panel's four tile steps (panel_chol_wide).  Iterates vs the oracle in the kernel's operation
     order (X = W^-1 G, Cholesky + triangular solves) rel <= 1e-8, and vs the
     reference's own order at the first iteration; the explicit-inverse order
     (a swept panel row in registers) stays limited to n <= 512."""

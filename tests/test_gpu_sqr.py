@@ -313,6 +313,11 @@ def test_sqr_optimal_control_n150(oracle):
     (160, 160, 256, [(0, 0, 16)] + [(1, 16 + 16 * i, 16) for i in range(15)], True),  # n, m, k at their limits
     (77, 0, 90, [(1, 0, 30), (1, 30, 29), (1, 59, 31)], False),     # ragged SOC cones, m = 0
     (129, 65, 140, [(0, 0, 140)], False),                           # LP: no modification, odd sizes
+    # beyond the LDS-packed factor (SqrLayout::gfac: the packed factors and the
+    # C chunk in the record)
+    (300, 120, 400, [(0, 0, 100)] + [(1, 100 * i, 100) for i in range(1, 4)], False),
+    (520, 200, 600, [(1, 0, 300), (1, 300, 300)], False),
+    (256, 256, 300, [(1, 0, 150), (1, 150, 150)], True),            # sing, m = n
 ])
 def test_sqr_workgroup_shapes_vs_oracle(oracle, n, m, k, cones, sing):
     rng = np.random.default_rng(n * 1000 + m * 10 + k)
@@ -348,6 +353,27 @@ def test_sqr_workgroup_shapes_vs_oracle(oracle, n, m, k, cones, sing):
                 ref = o[key]
                 assert np.abs(sl(got[key], q) - ref).max() <= tol * max(1.0, np.abs(ref).max()), (p, key, kap)
     assert ok >= B // 2
+
+
+def test_sqr_solve_socp_large_shape(oracle):
+    """solve_socp on the rank-update plugin beyond the old n, m <= 160, k <= 256
+    cap (the record-resident factors, the IPM's two-pass residuals for k > 256):
+    fixed-K trajectories vs the oracle's F_SQR IPM, rel <= 1e-8."""
+    n, m, k = 300, 40, 360
+    cones = [(0, 0, 60)] + [(1, 60 + 100 * i, 100) for i in range(3)]
+    B = 2
+    d = oracle.generate(cones, B, n, m, k, 0x534F4350 + 21)
+    for K in (1, 2):
+        r = oracle.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"], sing=np.zeros(B, np.uint8),
+                               params=oracle.Params(maxit=K, tol=0.0, flags=oracle.F_SQR))
+        hd = S.SqrHandle(cones, n, m, k, d["A"], d["G"], np.zeros(B, np.uint8))
+        g = hd.solve_socp(d["c"], d["b"], d["h"], maxit=K, tol=0.0)
+        assert (g["status"] == r["status"]).all() and (g["iters"] == r["iters"]).all()
+        for p in range(B):
+            for key, L in (("x", n), ("z", k), ("s", k)):
+                a_, b_ = g[key][p * L:(p + 1) * L], r[key][p * L:(p + 1) * L]
+                e = np.linalg.norm(a_ - b_) / np.linalg.norm(b_)
+                assert e <= 1e-8, (K, p, key, e)
 
 
 def test_sqr_workgroup_failures_isolated(oracle):
