@@ -92,7 +92,7 @@ enum : int {
 };
 constexpr int NKV = 17;
 #ifndef SOCP_SYRK_UBT
-#define SOCP_SYRK_UBT 0  // 1: the SYRK's U-row addresses from a launch-wide table
+#define SOCP_SYRK_UBT 1  // the SYRK's U-row addresses from a launch-wide table (0: from the codes)
 #endif
 // per-cone constants (SOC cones), recomputed by every scaling:
 //   MU = mu, IMU = 1/mu, WB0 = wbar_0, I1 = 1/(1+wbar_0), W2 = |wbar_1|^2,
@@ -1712,27 +1712,24 @@ struct Small {
     double ca, cb;
     int ub;  // LDS index of the cone's U row + cl
   };
-#if SOCP_SYRK_UBT
-  // (the lane ids of form_H, computed once for the whole product)
-  __device__ __forceinline__ XCoef genX_a(int pp, int g, int cl) {
-    const int row = 4 * pp + g;
+  // (UBT shapes: the lane ids of form_H, computed once for the whole product,
+  // and the U row from the launch's table)
+  __device__ __forceinline__ XCoef genX_a(int pp, int g_, int cl_) {
     XCoef c;
-    c.ca = LDS(CA + row);
-    c.cb = LDS(CBV + row);
-    c.ub = ubt(row) + cl;  // O_U + cone(row) * NPAD, from the launch's table
+    if constexpr (SH::UBT) {
+      const int row = 4 * pp + g_;
+      c.ca = LDS(CA + row);
+      c.cb = LDS(CBV + row);
+      c.ub = ubt(row) + cl_;  // O_U + cone(row) * NPAD
+    } else {
+      LANE_IDS();
+      const int row = 4 * pp + g;
+      c.ca = LDS(CA + row);
+      c.cb = LDS(CBV + row);
+      c.ub = O_U + (((int)LDS(O_RC + row)) >> 2) * NPAD + cl;
+    }
     return c;
   }
-#else
-  __device__ __forceinline__ XCoef genX_a(int pp, int, int) {
-    LANE_IDS();
-    const int row = 4 * pp + g;
-    XCoef c;
-    c.ca = LDS(CA + row);
-    c.cb = LDS(CBV + row);
-    c.ub = O_U + (((int)LDS(O_RC + row)) >> 2) * NPAD + cl;
-    return c;
-  }
-#endif
   __device__ __forceinline__ void genX_b(int pp, const XCoef& c, double (&X)[NQ]) {
     double u[NQ];
 #pragma unroll

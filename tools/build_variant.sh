@@ -19,7 +19,10 @@ for f in $GEN/inst_*.hip; do
   /opt/rocm/bin/hipcc $FLAGS -c $f -o $OBJ/$b.o > $OBJ/$b.log 2>&1 &
   pids+=($!)
 done
+# the C ABI too (host-side layout helpers such as small_lds_bytes see the flags)
+/opt/rocm/bin/hipcc $FLAGS -c $C/socp_api.hip -o $OBJ/socp_api.o > $OBJ/socp_api.log 2>&1 &
+pids+=($!)
 for p in "${pids[@]}"; do wait $p || { echo "compile failed"; cat $OBJ/*.log | tail -20; exit 1; }; done
 M=$R/socp.jl_amd/build/obj
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $LIB/libsocp.so $M/socp_api.o $M/socp_large.o $M/socp_large_gv.o $M/socp_sqr.o $M/socp_sqr_ipm.o $OBJ/inst_*.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $LIB/libsocp.so $OBJ/socp_api.o $M/socp_large.o $M/socp_large_gv.o $M/socp_sqr.o $M/socp_sqr_ipm.o $OBJ/inst_*.o
 echo "built $LIB/libsocp.so"
