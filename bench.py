@@ -408,7 +408,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="per CPU line (two lines)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-ingest", action="store_true",
-                    help="skip the PCIe-inclusive line (host batches through socp_ingest, N=1 only)")
+                    help="skip the PCIe-inclusive line (host batches through socp_ingest, N=1 only) and the "
+                         "other-mode summaries (explicit inverse, rank-update plugin): only the timed solver launches")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default: the newest profiles/rNN_pmc_traffic[_<config>].json")
     args = ap.parse_args()
@@ -533,7 +534,7 @@ def main():
         }
         if world == 1 and not args.no_ingest:
             line["ingest"] = ingest_line(S, cfg, B, K, tol, (c, A, b, G, h), args.steps, ctx)
-        if world == 1 and not args.explicit_inverse and not ref_rule:
+        if world == 1 and not args.explicit_inverse and not ref_rule and not args.no_ingest:
             # the other operation order on the same batch (never `value`): the
             # reference's explicit Li = H^-1 (SOCP_F_EXPLICIT_INVERSE); its own
             # line is `--explicit-inverse`
