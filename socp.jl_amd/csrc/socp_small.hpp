@@ -174,7 +174,10 @@ inline size_t small_lds_bytes(int NQ, int NP, int MQ) {
   const bool ubt = SOCP_SYRK_UBT && NQ * NP > 24 && NQ > 1;                   // Shape::UBT
   int total = O_FIXED + KS + NKV * KS + MPAD * LDA + 6 * NPAD + 6 * MPAD + ual + (tb_alias ? 0 : 16 * 17) +
               (ubt ? (KS + 1) / 2 : 0);
-  return (size_t)total * sizeof(double);
+#ifndef SOCP_DEV_LDS_PAD
+#define SOCP_DEV_LDS_PAD 0  // probe builds only: extra LDS bytes per wave to cap the waves per CU
+#endif
+  return (size_t)total * sizeof(double) + SOCP_DEV_LDS_PAD;
 }
 
 // Diagnostic phase timing (separate build, -DSOCP_DIAG): per-phase s_memtime
@@ -625,6 +628,9 @@ __device__ __forceinline__ double rsqrt_tile(double d) {
 #endif
 #ifndef SOCP_TILE_OKDIAG
 #define SOCP_TILE_OKDIAG 1  // the pivot test once per tile, on the diagonal of W (0: per pivot)
+#endif
+#ifndef SOCP_S_TILE
+#define SOCP_S_TILE 1  // m <= 16 Cholesky shapes: S^-1 = W'W from one factor_tile (0: Gauss-Jordan sweep)
 #endif
 #ifndef SOCP_TILE_INPLACE
 #define SOCP_TILE_INPLACE 1  // 0: copy back only registers > B (A/B builds)
@@ -2192,11 +2198,25 @@ struct Small {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (g + 4 * r == cl && cl >= m) Sv[0][r] = 1.0;
+#if SOCP_S_TILE
+      // S = L L' on one tile (potrf's pivot test), S^-1 = W'W with W = L^-1:
+      // one MFMA tile chain and four MFMAs instead of the 16-pivot sweep
+      bool okS = true;
+      if (!(SOCP_KO & 8)) {
+        d4 Ws;
+        factor_tile<TILE_INPL>(Sv[0], Ws, okS);
+        Sv[0] = mm<0>(Ws, Ws, (d4){0.0, 0.0, 0.0, 0.0});
+      }
+      clear_tb();
+      STAMP(SP_SCHUR);
+      if (!okS) return ST_CHOL_S;
+#else
       const bool okS = (SOCP_KO & 8) ? true : sweep<1, false>(Sv);
       clear_tb();
       STAMP(SP_SCHUR);
       if (!okS) return ST_CHOL_S;
       Sv[0] = -Sv[0];
+#endif
       return 0;
     }
     const bool okH = sweep<NQ, true>(T);
@@ -3260,7 +3280,10 @@ struct Small {
 // KM bit 0: the plugin-entry kernel (MODE_KKT / MODE_SETUP / MODE_SOLVEKKT)
 // instead of the solver; bit 1: the explicit-inverse variant (XI above)
 template <int NQ, int NP, int MQ, int KM>
-__global__ void __launch_bounds__(64, 1) socp_small_kernel(SmallArgs args) {
+#ifndef SOCP_DEV_MINW
+#define SOCP_DEV_MINW 1  // probe builds only: waves per SIMD the register allocation must allow
+#endif
+__global__ void __launch_bounds__(64, KM == 0 ? SOCP_DEV_MINW : 1) socp_small_kernel(SmallArgs args) {
   Small<NQ, NP, MQ, (KM & 2) != 0> S(args);
   S.init_tables();
   STAMP_START_S(S);

@@ -22,6 +22,10 @@ from socp_amd.configs import CONFIGS  # noqa: E402
 cfg = CONFIGS[sys.argv[1]]
 reps = int(sys.argv[2])
 paths = sys.argv[3:]
+if os.environ.get("AB_SHAPE"):  # probe shapes: "n,m,k" with POC(0, k/2) + SOC(k/2, k - k/2)
+    import dataclasses
+    n_, m_, k_ = map(int, os.environ["AB_SHAPE"].split(","))
+    cfg = dataclasses.replace(cfg, n=n_, m=m_, k=k_, cones=((0, 0, k_ // 2), (1, k_ // 2, k_ - k_ // 2)))
 B, n, m, k = cfg.batch, cfg.n, cfg.m, cfg.k
 if os.environ.get("AB_BATCH"):
     B = int(os.environ["AB_BATCH"])

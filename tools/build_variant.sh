@@ -7,11 +7,11 @@ set -e
 name=$1; extra=$2
 R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/socp.jl_amd/csrc
-GEN=$R/socp.jl_amd/build/gen_dev
+GEN=$R/socp.jl_amd/build/gen_v_$name
 OBJ=$R/socp.jl_amd/build/obj_v_$name
 LIB=$R/socp.jl_amd/lib/v_$name
 mkdir -p $GEN $OBJ $LIB
-SOCP_DEV_VARIANTS=1 python3 $C/gen_inst.py $GEN > /dev/null
+SOCP_DEV_VARIANTS=${DEV_VARIANTS:-1} python3 $C/gen_inst.py $GEN > /dev/null
 FLAGS="-I$C -O3 -std=c++17 -ffp-contract=fast-honor-pragmas -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-use-amdgpu-trackers=1 -mllvm -amdgpu-disable-unclustered-high-rp-reschedule=1 --offload-arch=gfx950 -fPIC -Wno-unused-function -Wno-unused-variable $extra"
 pids=()
 for f in $GEN/inst_*.hip; do
