@@ -223,6 +223,12 @@ __device__ __forceinline__ double dot_strided(const double* p, int64_t stride, c
 #define SQR_GU 16
 #endif
 
+#ifndef SQR_S_MFMA
+#define SQR_S_MFMA 1  // 0: S = C'C one entry per lane (dot products out of LDS)
+#endif
+#ifndef SQR_S_REGS
+#define SQR_S_REGS 1  // 0: chol(S) in LDS for every m (m <= 16: rows of S in registers)
+#endif
 // 1/sqrt(x) from v_rsq_f64 refined by two Newton steps (to within an ulp or
 // two; x < 0 or NaN gives NaN, which the callers' status checks catch; +-0 and
 // +inf give the IEEE +-inf and 0, not the 0 * inf NaN of the refinement)
@@ -569,11 +575,68 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
       wsync();
       SQ_STAMP(4);
       double* Sm = lds + L.o_S;
+#if SQR_S_MFMA
+      // S = C'C by lower 16 x 16 tiles on f64 MFMA (k-steps of four rows of C)
+      {
+        const int g = lane >> 4, cl = lane & 15;
+        const int MT = (m + 15) / 16;
+        for (int I = 0; I < MT; ++I)
+          for (int J = 0; J <= I; ++J) {
+            d4v acc = {0.0, 0.0, 0.0, 0.0};
+            const int ci = 16 * I + cl, cj = 16 * J + cl;
+            for (int s4 = 0; s4 < n; s4 += 4) {
+              const int row = s4 + g;
+              const double u = (row < n && ci < m) ? Cm[ci * L.ldl + row] : 0.0;
+              const double v = (row < n && cj < m) ? Cm[cj * L.ldl + row] : 0.0;
+              acc = __builtin_amdgcn_mfma_f64_16x16x4f64(u, v, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int R = 16 * I + g + 4 * r, Cc = 16 * J + cl;
+              if (R < m && Cc < m && R >= Cc) Sm[Cc * L.ldm + R] = acc[r];
+            }
+          }
+        wsync();
+      }
+#else
       // one entry (r, q), r >= q, per lane: independent dot products
       for (int e = lane; e < m * m; e += 64) {
         const int r = e % m, q = e / m;
         if (r >= q) Sm[q * L.ldm + r] = dot_strided(Cm + r * L.ldl, 1, Cm + q * L.ldl, n);
       }
+#endif
+#if SQR_S_REGS
+      if (m <= 16) {
+        // chol(S) with the rows of S in registers (lane i: row i), right-looking
+        // as the register Cholesky of H above; the lower triangle back to Sm
+        double sr[16], rdv = 1.0;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) sr[l] = (lane < m && l <= lane) ? Sm[l * L.ldm + lane] : 0.0;
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          if (j >= m) continue;  // wave-uniform
+          const double d = bcast(sr[j], j);
+          bad |= !(d > 0.0);
+          const double ir = rsqrt_nr(d), r = d * ir;
+          if (lane == j) {
+            sr[j] = r;
+            rdv = ir;
+          } else if (lane > j) {
+            sr[j] *= ir;
+          }
+#pragma unroll
+          for (int l = j + 1; l < 16; ++l) sr[l] -= sr[j] * bcast(sr[j], l);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int l = 0; l < 16; ++l)
+          if (lane < m && l <= lane) Sm[l * L.ldm + lane] = sr[l];
+        if (lane < m) lds[L.o_rdgs + lane] = rdv;
+        wsync();
+        if (bad) status = SQR_CHOL_S;
+      } else
+#endif
       if (!chol_lds(Sm, L.ldm, m, lds + L.o_rdgs, lane)) status = SQR_CHOL_S;
       SQ_STAMP(5);
     }
