@@ -248,9 +248,11 @@ int socp_dense_destroy(socp_dense* h);
  *                        B x ncones) of the last setup_iter.
  * CHOLMOD's fill-reducing permutation and supernodal LDL' are replaced by a
  * dense factor: results agree with the reference to rounding, not bitwise.
- * Shapes: n, m <= 160, k <= 256, <= 64 cones, within 160 KiB of LDS
- * (socp_sqr_supported): one wavefront per problem for n, m <= 64, one
- * 256-thread workgroup (the factor packed in LDS) above.  Flags and
+ * Shapes: n, m <= 1024, k <= 4096, <= 64 cones, the problem's vectors
+ * within 160 KiB of LDS (socp_sqr_supported): one wavefront per problem for
+ * n, m <= 64, one 256-thread workgroup above -- its factors packed in LDS,
+ * or in the per-problem record when they and a right-hand-side chunk exceed
+ * the LDS (n, m beyond about 160).  Flags and
  * host/device pointer semantics as socp_dense_*. */
 typedef struct socp_sqr socp_sqr;
 int socp_sqr_supported(const socp_dims* dims);

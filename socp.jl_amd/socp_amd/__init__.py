@@ -346,8 +346,8 @@ class SqrHandle(DenseHandle):
     sqrscalings.jl).  ``setup_iter(s, z)`` computes W^-2 = D + uu' - vv',
     factors G'DG (+A'A), applies one rank-1 update (G'u) and one downdate (G'v)
     per SOC cone and factors S; ``solve_kkt`` solves by triangular solves.
-    Same call conventions as DenseHandle; n, m <= 160, k <= 256 (one wavefront
-    per problem up to n, m = 64, one workgroup above)."""
+    Same call conventions as DenseHandle; n, m <= 1024, k <= 4096 (one
+    wavefront per problem up to n, m = 64, one workgroup above)."""
 
     _pfx = "socp_sqr"
 
