@@ -396,9 +396,16 @@ int socp_allgather_outcomes(socp_comm* comm, int64_t batch, const int32_t* statu
                             const double* res, socp_outcome* out);
 
 /* Timing of the last solve's main kernel, measured with HIP events on the
- * context's stream (milliseconds), and its name. */
+ * context's stream (milliseconds), and its name.  socp_last_kernel_ms waits
+ * for that launch. */
 int socp_last_kernel_ms(socp_ctx* ctx, float* ms);
 const char* socp_last_kernel_name(socp_ctx* ctx);
+/* The main-kernel times of the context's last min(n, 64) timed launches,
+ * oldest first, into ms[]; returns how many were written (< 0: error).  Each
+ * launch records its own event pair, so a run of launches is timed without a
+ * host synchronisation between them (bench.py's timed steps); the call waits
+ * for the newest one. */
+int socp_kernel_times(socp_ctx* ctx, float* ms, int n);
 
 /* Testing hook (not part of the reference surface; diagnostic build
  * libsocp_diag.so only): when set to a device buffer of

@@ -60,7 +60,12 @@ struct socp_ctx {
   int device = 0;
   hipStream_t own = nullptr;     // created by socp_ctx_create
   hipStream_t stream = nullptr;  // where work goes: `own`, or the caller's (socp_ctx_set_stream)
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // timing pair (socp_last_kernel_ms)
+  // timing pairs around the solver launches, a ring of NTIME so that a run of
+  // launches can be timed without a host synchronisation between them
+  // (socp_last_kernel_ms, socp_kernel_times)
+  static constexpr int NTIME = 64;
+  hipEvent_t tev0[NTIME] = {}, tev1[NTIME] = {};
+  int64_t tlaunches = 0;
   hipEvent_t evh = nullptr;                 // stream hand-off (ctx_switch_stream), never a timing event
   int num_cu = 0;
   float last_ms = 0.f;
@@ -95,8 +100,10 @@ static void ctx_free(socp_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->own && c->own != c->stream) (void)hipStreamSynchronize(c->own);
   for (auto& b : c->buf) b.release();
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (int i = 0; i < socp_ctx::NTIME; ++i) {
+    if (c->tev0[i]) (void)hipEventDestroy(c->tev0[i]);
+    if (c->tev1[i]) (void)hipEventDestroy(c->tev1[i]);
+  }
   if (c->evh) (void)hipEventDestroy(c->evh);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -123,8 +130,10 @@ extern "C" int socp_ctx_create(int device, socp_ctx** out) {
   if ((e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) != hipSuccess)
     return bail(e, "hipStreamCreateWithFlags");
   c->stream = c->own;
-  if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return bail(e, "hipEventCreate");
-  if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return bail(e, "hipEventCreate");
+  for (int i = 0; i < socp_ctx::NTIME; ++i) {
+    if ((e = hipEventCreate(&c->tev0[i])) != hipSuccess) return bail(e, "hipEventCreate");
+    if ((e = hipEventCreate(&c->tev1[i])) != hipSuccess) return bail(e, "hipEventCreate");
+  }
   if ((e = hipEventCreateWithFlags(&c->evh, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
   *out = c;
   return 0;
@@ -165,12 +174,38 @@ extern "C" int socp_ctx_sync(socp_ctx* c) {
 
 extern "C" void* socp_ctx_stream(socp_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+// the timing pair of the next launch (recorded by timing_begin / timing_end)
+static hipError_t timing_begin(socp_ctx* c) {
+  return hipEventRecord(c->tev0[c->tlaunches % socp_ctx::NTIME], c->stream);
+}
+static hipError_t timing_end(socp_ctx* c) {
+  const hipError_t e = hipEventRecord(c->tev1[c->tlaunches % socp_ctx::NTIME], c->stream);
+  if (e == hipSuccess) ++c->tlaunches;
+  return e;
+}
+
 extern "C" int socp_last_kernel_ms(socp_ctx* c, float* ms) {
   if (!c || !ms) return fail(SOCP_E_INVALID, "NULL argument");
-  HIPCHK(hipEventSynchronize(c->ev1));
-  HIPCHK(hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  if (c->tlaunches == 0) return fail(SOCP_E_INVALID, "no timed launch on this context");
+  const int i = (int)((c->tlaunches - 1) % socp_ctx::NTIME);
+  HIPCHK(hipEventSynchronize(c->tev1[i]));
+  HIPCHK(hipEventElapsedTime(&c->last_ms, c->tev0[i], c->tev1[i]));
   *ms = c->last_ms;
   return 0;
+}
+
+extern "C" int socp_kernel_times(socp_ctx* c, float* ms, int n) {
+  if (!c || !ms || n < 0) return fail(SOCP_E_INVALID, "NULL argument or n < 0");
+  int64_t cnt = c->tlaunches < n ? c->tlaunches : n;
+  if (cnt > socp_ctx::NTIME) cnt = socp_ctx::NTIME;
+  if (cnt == 0) return 0;
+  HIPCHK(hipEventSynchronize(c->tev1[(c->tlaunches - 1) % socp_ctx::NTIME]));
+  for (int64_t j = 0; j < cnt; ++j) {
+    const int i = (int)((c->tlaunches - cnt + j) % socp_ctx::NTIME);
+    HIPCHK(hipEventElapsedTime(&ms[j], c->tev0[i], c->tev1[i]));
+  }
+  c->last_ms = ms[cnt - 1];
+  return (int)cnt;
 }
 extern "C" const char* socp_last_kernel_name(socp_ctx* c) { return c ? c->last_name : ""; }
 
@@ -296,9 +331,9 @@ static int launch_small(socp_ctx* ctx, SmallArgs& args, const SmallVariant* v) {
   HIPCHK(hipMemsetAsync(args.counter, 0, sizeof(int32_t), ctx->stream));
   args.stamps = g_stamps;
   void* kargs[] = {&args};
-  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIPCHK(timing_begin(ctx));
   HIPCHK(hipLaunchKernel(kern, dim3((unsigned)blocks), dim3(64), kargs, lds, ctx->stream));
-  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  HIPCHK(timing_end(ctx));
   ctx->last_name = xi ? (solver ? v->xi_name : v->xi_kkt_name) : (solver ? v->name : v->kkt_name);
   return 0;
 }
@@ -327,9 +362,9 @@ static int launch_large(socp_ctx* ctx, const SmallArgs& a, double* rec = nullptr
   la.rec = rec;
   HIPCHK(hipMemsetAsync(a.counter, 0, sizeof(int32_t), ctx->stream));
   void* kargs[] = {&la};
-  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIPCHK(timing_begin(ctx));
   HIPCHK(hipLaunchKernel(kern, dim3((unsigned)grid), dim3(512), kargs, lds, ctx->stream));
-  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  HIPCHK(timing_end(ctx));
   ctx->last_name = large_kernel_name(xi, gv);
   return 0;
 }
@@ -963,10 +998,10 @@ static int sqr_launch(socp_sqr* h, const SqrArgs& a, bool setup, bool timed = tr
   SqrArgs la = a;
   la.stamps = g_stamps;
   void* kargs[] = {&la};
-  if (timed) HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  if (timed) HIPCHK(timing_begin(ctx));
   const int nt = sqr_block_threads(a.n, a.m);
   HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(nt), kargs, h->lds, ctx->stream));
-  if (timed) HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  if (timed) HIPCHK(timing_end(ctx));
   ctx->last_name = nt > 64 ? (setup ? "socp_sqr_setup_wg_kernel" : "socp_sqr_solve_wg_kernel")
                            : (setup ? "socp_sqr_setup_kernel" : "socp_sqr_solve_kernel");
   return 0;
@@ -1113,7 +1148,7 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
     HIPCHK(hipLaunchKernel(sqr_ipm_kernel_ptr(which), grid, blk, which == 4 ? args2 : args1, lds, ctx->stream));
     return 0;
   };
-  HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+  HIPCHK(timing_begin(ctx));
   // initial point: the KKT system with W = I (s = z = e), then the shift
   TRY(ipm(0, 0));
   TRY(sqr_launch(h, su, true, false));
@@ -1140,7 +1175,7 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
     }
   }
   if (res) TRY(ipm(5, 0));
-  HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+  HIPCHK(timing_end(ctx));
   ctx->last_name = "socp_sqr_solve_socp";
   if (dev) {
     HIPCHK(hipMemcpyAsync(x, ia.x, (size_t)B * n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));

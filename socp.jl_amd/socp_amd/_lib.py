@@ -24,7 +24,7 @@ EXPORTED = [
     "socp_last_error", "socp_version", "socp_params_default", "socp_ctx_create",
     "socp_ctx_destroy", "socp_ctx_sync", "socp_ctx_stream", "socp_ctx_set_stream", "socp_ctx_reset_stream", "socp_supported",
     "socp_batch_solve", "socp_batch_solve_ex", "socp_batch_kkt_solve", "socp_generate",
-    "socp_last_kernel_ms", "socp_last_kernel_name", "socp_debug_set_kkt_dump",
+    "socp_last_kernel_ms", "socp_last_kernel_name", "socp_kernel_times", "socp_debug_set_kkt_dump",
     "socp_debug_set_stamps", "socp_pack_csc", "socp_comm_unique_id", "socp_comm_init",
     "socp_comm_destroy", "socp_allgather_status", "socp_allgather_outcomes",
     "socp_dense_create", "socp_dense_setup_iter", "socp_dense_solve_kkt", "socp_dense_h2d_bytes",
@@ -102,6 +102,7 @@ def load():
     L.socp_batch_kkt_solve.argtypes = common + [dp, dp, u8p] + [dp] * 2 + [dp] * 4 + [dp] * 4 + [i32p, C.c_int32]
     L.socp_generate.argtypes = common + [C.c_uint64, C.c_int64] + [dp] * 5
     L.socp_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    L.socp_kernel_times.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
     L.socp_last_kernel_name.argtypes = [vp]
     L.socp_last_kernel_name.restype = C.c_char_p
     L.socp_debug_set_kkt_dump.argtypes = [vp]
@@ -208,6 +209,14 @@ class Context:
         v = C.c_float()
         check(load().socp_last_kernel_ms(self.handle, C.byref(v)))
         return float(v.value)
+
+    def kernel_times(self, n: int) -> list:
+        """Main-kernel times (ms) of the last min(n, 64) timed launches, oldest
+        first (socp_kernel_times): no host synchronisation between launches."""
+        buf = (C.c_float * max(n, 1))()
+        got = load().socp_kernel_times(self.handle, buf, n)
+        check(min(got, 0))
+        return [float(buf[i]) for i in range(got)]
 
     def last_kernel_name(self) -> str:
         return load().socp_last_kernel_name(self.handle).decode()
