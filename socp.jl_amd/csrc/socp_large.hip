@@ -30,6 +30,25 @@
 #define SOCP_MULTI_WAVE 1  // LANE_IDS / factor_tile: lanes of 8-wavefront workgroups
 #include "socp_kernels.hpp"
 
+// Tuning builds only (never the product): SOCP_LREP bit b runs an idempotent
+// phase of the blocked kernel twice, so that the time and the PMC traffic of
+// one instance are the build's difference to the product -- 1 X = W^-1 G,
+// 2 the SYRK, 4 the solves' G'v, 8 their G v, 16 their triangular solves,
+// 32 Z = L^-1 A' and S = Z'Z, 64 the residuals' G pass
+#ifndef SOCP_LREP
+#define SOCP_LREP 0
+#endif
+#define LREP(b) ((SOCP_LREP & (b)) ? 2 : 1)
+#ifndef SOCP_LG_CATCH_SPLIT
+#define SOCP_LG_CATCH_SPLIT 1  // chol_nb: split the last panels' catch-up blocks by 16-column groups
+#endif
+#ifndef SOCP_LG_SYRK_UNROLL
+#define SOCP_LG_SYRK_UNROLL 1  // blk_gemm's k loop (16 rows per step)
+#endif
+#ifndef SOCP_LG_ZU
+#define SOCP_LG_ZU 8  // Z = L^-1 A' update: 4-row k-steps per batch of loads (P0 is a multiple of 64; 16: the same time)
+#endif
+
 namespace socp {
 namespace lg {
 
@@ -639,6 +658,7 @@ struct Large {
   __device__ __forceinline__ void blk_gemm(d4 (&acc)[4][4], gcdbl* P, gcdbl* Q, int ld, int I0,
                                            int J0, int kr, bool same, int qs) {
     const int g = lane >> 4, cl = lane & 15;
+#pragma unroll SOCP_LG_SYRK_UNROLL
     for (int k0 = 0; k0 < kr; k0 += 16) {
       double av[4][4], bv[4][4];
 #pragma unroll
@@ -715,6 +735,47 @@ struct Large {
           for (int b_ = 0; b_ < 4; ++b_)
             if (!LO || b_ >= a_) acc[a_][b_] = mfma(av[a_][s], bv[b_][s], acc[a_][b_]);
     }
+  }
+  // one 16-column group a_ of the block (acc[a_][*] of gram_blkT): the same
+  // MFMAs in the same order, so a block split into its four column groups over
+  // four wavefronts gives gram_blkT's result bit for bit
+  template <bool LO = false>
+  __device__ __forceinline__ void gram_colT(d4 (&acc)[4], gcdbl* Y, int ld, int I0, int J0, gcdbl* fv, int a_) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll 2
+    for (int k0 = 0; k0 < 64; k0 += 16) {
+      double av[4], bv[4][4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        gcdbl* row = Y + (int64_t)(k0 + 4 * s + g) * ld;
+        av[s] = fv[k0 + 4 * s + g] * row[J0 + 16 * a_ + cl];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bv[t][s] = row[I0 + 16 * t + cl];
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int b_ = 0; b_ < 4; ++b_)
+          if (!LO || b_ >= a_) acc[b_] = mfma(av[s], bv[b_][s], acc[b_]);
+    }
+  }
+  template <bool LO = false>
+  __device__ __forceinline__ void load_colT(d4 (&acc)[4], gcdbl* M, int ld, int I0, int J0, int a_) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int b_ = 0; b_ < 4; ++b_)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc[b_][r] = (LO && b_ < a_) ? 0.0 : M[(int64_t)(J0 + 16 * a_ + g + 4 * r) * ld + I0 + 16 * b_ + cl];
+  }
+  template <bool LO = false>
+  __device__ __forceinline__ void store_colT(const d4 (&acc)[4], gdbl* M, int ld, int I0, int J0, int a_) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int b_ = 0; b_ < 4; ++b_)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!LO || b_ >= a_) M[(int64_t)(J0 + 16 * a_ + g + 4 * r) * ld + I0 + 16 * b_ + cl] = acc[b_][r];
   }
   template <bool LO = false>
   __device__ __forceinline__ void load_blkT(d4 (&acc)[4][4], gcdbl* M, int ld, int I0, int J0) {
@@ -1296,7 +1357,24 @@ struct Large {
   template <int nb>
   __device__ bool chol_nb(gdbl* M, int ld) {
     for (int P = 0; P < nb; ++P) {
-      if (P > 0) {
+      if (P > 0 && SOCP_LG_CATCH_SPLIT && 2 * (nb - P) <= NW) {
+        // few blocks left: each block's catch-up split into its four 16-column
+        // groups, one per wavefront (bitwise the whole-block result)
+        for (int it = wv; it < 4 * (nb - P); it += NW) {
+          const int t = P + it / 4, a_ = it % 4;
+          d4 acc[4];
+          if (t == P) {
+            load_colT<true>(acc, M, ld, 64 * t, 64 * P, a_);
+            for (int Q = 0; Q < P; ++Q) gram_colT<true>(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q, a_);
+            store_colT<true>(acc, M, ld, 64 * t, 64 * P, a_);
+          } else {
+            load_colT(acc, M, ld, 64 * t, 64 * P, a_);
+            for (int Q = 0; Q < P; ++Q) gram_colT(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q, a_);
+            store_colT(acc, M, ld, 64 * t, 64 * P, a_);
+          }
+        }
+        BAR();
+      } else if (P > 0) {
         for (int t = P + wv; t < nb; t += NW) {
           d4 acc[4][4];
           if (t == P) {
@@ -1496,13 +1574,21 @@ struct Large {
         d4 acc0, acc1 = zero;
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc0[r] = Ap[(int64_t)(P0 + 16 * ta + g + 4 * r) * MP + 16 * tb + cl];
-        for (int y0 = 0; y0 < P0; y0 += 8) {
-          const double a0 = Lm[(int64_t)(y0 + g) * ld + P0 + 16 * ta + cl];
-          const double b0 = Tm[(int64_t)(y0 + g) * MP + 16 * tb + cl];
-          const double a1 = Lm[(int64_t)(y0 + 4 + g) * ld + P0 + 16 * ta + cl];
-          const double b1 = Tm[(int64_t)(y0 + 4 + g) * MP + 16 * tb + cl];
-          acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc0, 0, 0, 1);  // -= L Z
-          acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc1, 0, 0, 1);
+        // 4 SOCP_LG_ZU rows per round, their loads issued before the MFMAs (one
+        // memory round trip per 32 rows instead of per 8); acc0 / acc1 take the
+        // same rows in the same order as before
+        for (int y0 = 0; y0 < P0; y0 += 4 * SOCP_LG_ZU) {
+          double a[SOCP_LG_ZU], b[SOCP_LG_ZU];
+#pragma unroll
+          for (int u = 0; u < SOCP_LG_ZU; ++u) {
+            a[u] = Lm[(int64_t)(y0 + 4 * u + g) * ld + P0 + 16 * ta + cl];
+            b[u] = Tm[(int64_t)(y0 + 4 * u + g) * MP + 16 * tb + cl];
+          }
+#pragma unroll
+          for (int u = 0; u < SOCP_LG_ZU; u += 2) {
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc0, 0, 0, 1);  // -= L Z
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u + 1], b[u + 1], acc1, 0, 0, 1);
+          }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) Rs[(int64_t)(16 * ta + g + 4 * r) * MP + 16 * tb + cl] = acc0[r] + acc1[r];
@@ -1512,11 +1598,16 @@ struct Large {
         LANE_IDS();
         const int ta = tt / MT, tb = tt - ta * MT, i = 16 * ta + cl;
         d4 acc = zero;
-        for (int x0 = 0; x0 <= 16 * ta + 12; x0 += 4) {  // E is lower: x <= i
-          const int x = x0 + g;
-          const double av = (x <= i) ? Lm[(int64_t)(P0 + x) * ld + P0 + i] : 0.0;
-          const double bv = Rs[(int64_t)x * MP + 16 * tb + cl];
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        for (int x0 = 0; x0 <= 16 * ta + 12; x0 += 16) {  // E is lower: x <= i; 4 steps per round trip
+          double av[4], bv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int x = x0 + 4 * u + g;
+            av[u] = (x <= i) ? Lm[(int64_t)(P0 + x) * ld + P0 + i] : 0.0;
+            bv[u] = Rs[(int64_t)x * MP + 16 * tb + cl];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) Tm[(int64_t)(P0 + 16 * ta + g + 4 * r) * MP + 16 * tb + cl] = acc[r];
@@ -1771,19 +1862,24 @@ struct Large {
   __device__ int factor(bool addAA, bool h_only) {
     LSTAMP(SP_OTHER);
     const bool stg = form_X_fast_ok() && staged_ok();
-    if (!form_X_fast(stg)) form_X();
+    for (int rep = 0; rep < LREP(1); ++rep)
+      if (!form_X_fast(stg)) form_X();
     LSTAMP(SP_U);
-    if (stg)
-      form_H_staged(addAA);
-    else
-      form_H(addAA);
+    for (int rep = 0; rep < LREP(2); ++rep) {
+      if (stg)
+        form_H_staged(addAA);
+      else
+        form_H(addAA);
+    }
     LSTAMP(SP_SYRK);
     if constexpr (CHOL) {
     if (!chol(Hm, L.NPAD)) return ST_CHOL_H;
     if (h_only) return 0;
     LSTAMP(SP_SWEEP_H);
-    chol_fwd_multi(Hm, L.NPAD);
-    form_S_gram();
+    for (int rep = 0; rep < LREP(32); ++rep) {
+      chol_fwd_multi(Hm, L.NPAD);
+      form_S_gram();
+    }
     LSTAMP(SP_SCHUR);
     } else {
     if (!sweep(Hm, L.NPAD)) return ST_CHOL_H;
@@ -2054,11 +2150,25 @@ struct Large {
       LV(p1 + wv * 64 + lane) = acc;
       LDS_BAR();
       acc = 0.0;
-      for (int x = wv; x < 64 && P0 + x < n; x += NW) {
-        double r = LV(vin + P0 + x);
+      {
+        // the panel's 64 / NW columns of this wavefront: their loads first
+        // (one memory round trip), then the same FMA chain as before
+        constexpr int XW = 64 / NW;
+        double lx[XW];
 #pragma unroll
-        for (int w = 0; w < NW; ++w) r -= LV(p1 + w * 64 + x);
-        if (x <= lane && i < n) acc = fma(Lm[(int64_t)(P0 + x) * ld + i], r, acc);
+        for (int j = 0; j < XW; ++j) {
+          const int x = wv + NW * j;
+          lx[j] = (P0 + x < n && x <= lane && i < n) ? Lm[(int64_t)(P0 + x) * ld + i] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < XW; ++j) {
+          const int x = wv + NW * j;
+          if (P0 + x >= n) break;  // wave-uniform
+          double r = LV(vin + P0 + x);
+#pragma unroll
+          for (int w = 0; w < NW; ++w) r -= LV(p1 + w * 64 + x);
+          if (x <= lane && i < n) acc = fma(lx[j], r, acc);
+        }
       }
       LV(p2 + wv * 64 + lane) = acc;
       LDS_BAR();
@@ -2082,6 +2192,7 @@ struct Large {
       const int P0 = 64 * P;
       for (int i = 4 * wv + q; i < 64; i += 4 * NW) {
         double acc = 0.0;
+#pragma unroll 4
         for (int x = P0 + 64 + c; x < n; x += 16) acc = fma(Lm[(int64_t)(P0 + i) * ld + x], LV(vout + x), acc);
         acc = row16_sum(acc);
         if (c == 0) LV(p1 + i) = (P0 + i < n) ? LV(vin + P0 + i) - acc : 0.0;
@@ -2117,7 +2228,8 @@ struct Large {
 
   // rd = A'y + G'z + c, rp = Ax - b, rz = Gx + s - h (solver.jl:109-118)
   __device__ void residuals(double& nd, double& np_, double& gap) {
-    const bool merged = gemv_GtG(Z_, TN, X_, S_, H_, DZ);  // G'z and Gx + s - h in one G pass
+    bool merged = false;
+    for (int rep = 0; rep < LREP(64); ++rep) merged = gemv_GtG(Z_, TN, X_, S_, H_, DZ);  // G'z and Gx + s - h in one G pass
     if (!merged) gemv_Gt(Z_, TN, -1);
     double d2 = 0.0;
     for (int j = tid; j < n; j += NTH) {
@@ -2139,7 +2251,7 @@ struct Large {
   // (init: -cy); cx = Li (n0 + A'm0), taken as Li n0 + (Li A') m0; k1 = G cx - k2.
   // In: RD RP T2 K2.  Out: RX RY K1.
   __device__ void solve_matrix_part(bool init) {
-    gemv_Gt(T2, N0, RD);
+    for (int rep = 0; rep < LREP(4); ++rep) gemv_Gt(T2, N0, RD);
     if (sing) {
       for (int j = tid; j < n; j += NTH) LV(N0 + j) = LV(N0 + j) + At_dot(RP, j);
       BAR();
@@ -2147,7 +2259,7 @@ struct Large {
     if constexpr (CHOL) {
     // Li = L^-T L^-1: u = L^-1 n0; m0 = A Li n0 - dy = Z'u - dy; cy = S^-1 m0;
     // cx = Li (n0 + A'm0) = L^-T (u + Z m0)
-    trsv_fwd(Hm, L.NPAD, N0, TN, n);
+    for (int rep = 0; rep < LREP(16); ++rep) trsv_fwd(Hm, L.NPAD, N0, TN, n);
     mat_mv(Tm, TN, RP, M0);
     if (L.MPAD > 64 * LARGE_NB_MAX) {  // S = L_S L_S' (factor() factors S beyond the sweep's reach)
       trsv_fwd(Sm, L.MPAD, M0, M0, m);
@@ -2158,7 +2270,7 @@ struct Large {
     for (int r = tid; r < m; r += NTH) LV(M0 + r) = (sing && !init) ? LV(RP + r) - LV(RY + r) : -LV(RY + r);
     BAR();
     z_mv_add(TN, M0, N0);
-    trsv_bwd(Hm, L.NPAD, N0, RX, n);
+    for (int rep = 0; rep < LREP(16); ++rep) trsv_bwd(Hm, L.NPAD, N0, RX, n);
     } else {
     symv(Hm, L.NPAD, N0, TN);
     A_mv(TN, RP, M0);
@@ -2174,7 +2286,7 @@ struct Large {
     }
     BAR();
     }
-    gemv_G(RX, -1, K2, K1);
+    for (int rep = 0; rep < LREP(8); ++rep) gemv_G(RX, -1, K2, K1);
   }
 
   // ------------------------------------------------------------- driver
