@@ -862,19 +862,32 @@ struct Large {
     const int NPD = L.NPAD;
     const int KP = L.KP, ln = lane, kk = k, nn = n;
     const int fx = L.o_fx + wv * 64;  // [0,32): del[u][c], [32,64): head value g0[u][c]
-    for (int j0 = FX_CG * wv; j0 < L.NPAD; j0 += FX_CG * NW) {
-      const int nl = nn - j0;
-      gcdbl* g0p = Gp + (int64_t)(j0 < nn ? j0 : 0) * kk;
-      gdbl* x0 = Xw + (int64_t)j0 * KP;
-      double gv[FX_CG][FX_R], wbr[FX_R];
+    double wbr[FX_R];
+#pragma unroll
+    for (int r = 0; r < FX_R; ++r) {
+      const int row = ln + 64 * r;
+      wbr[r] = (r < R && row < kk) ? LV(WB + row) : 0.0;
+    }
+    // columns j0 .. j0 + FX_CG - 1 of G into gv (dead columns read column 0)
+    auto load_cols = [&](double (&dst)[FX_CG][FX_R], int j0_) {
+      const int nl_ = nn - j0_;
+      gcdbl* gp = Gp + (int64_t)(j0_ < nn ? j0_ : 0) * kk;
 #pragma unroll
       for (int r = 0; r < FX_R; ++r) {
         const int row = ln + 64 * r;
         const bool in = r < R && row < kk;
-        wbr[r] = in ? LV(WB + row) : 0.0;
 #pragma unroll
-        for (int u = 0; u < FX_CG; ++u) gv[u][r] = in ? g0p[(int64_t)(u < nl ? u : 0) * kk + row] : 0.0;
+        for (int u = 0; u < FX_CG; ++u) dst[u][r] = in ? gp[(int64_t)(u < nl_ ? u : 0) * kk + row] : 0.0;
       }
+    };
+    // (the next group's loads issued before this group's reductions, from a
+    // second buffer, measured 1 % slower at C4)
+    double gv[FX_CG][FX_R];
+    for (int j0 = FX_CG * wv; j0 < L.NPAD; j0 += FX_CG * NW) {
+      const int nl = nn - j0;
+      gcdbl* g0p = Gp + (int64_t)(j0 < nn ? j0 : 0) * kk;
+      gdbl* x0 = Xw + (int64_t)j0 * KP;
+      load_cols(gv, j0);
       // per SOC cone: del = sum over the tail of wbar_i G_ij
 #pragma unroll
       for (int ci = 0; ci < FX_NC; ++ci) {
@@ -890,12 +903,24 @@ struct Large {
 #pragma unroll
           for (int u = 0; u < FX_CG; ++u) pd[u] = fma(w, gv[u][r], pd[u]);
         }
+        // the head value G[o][j0 + u] is already in a register (row o of the
+        // loaded columns: lane o % 64, slot o / 64): a readlane instead of a
+        // global load per column and cone on the wave's critical path
+        const int ro = o >> 6, lo = o & 63;
 #pragma unroll
         for (int u = 0; u < FX_CG; ++u) {
+          double gh = 0.0;
+          if constexpr (!XI) {  // (the explicit-inverse kernel spills with it: a global load there)
+#pragma unroll
+            for (int r = 0; r < FX_R; ++r)
+              if (r == ro) gh = readlane_d(gv[u][r], lo);  // wave-uniform branch
+          } else {
+            gh = g0p[(int64_t)(u < nl ? u : 0) * kk + o];
+          }
           const double del = wave_sum(pd[u]);
           if (ln == 0) {
             LV(fx + u * FX_NC + ci) = del;
-            LV(fx + 32 + u * FX_NC + ci) = g0p[(int64_t)(u < nl ? u : 0) * kk + o];
+            LV(fx + 32 + u * FX_NC + ci) = gh;
           }
         }
       }
