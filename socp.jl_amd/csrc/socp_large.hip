@@ -34,7 +34,8 @@
 // phase of the blocked kernel twice, so that the time and the PMC traffic of
 // one instance are the build's difference to the product -- 1 X = W^-1 G,
 // 2 the SYRK, 4 the solves' G'v, 8 their G v, 16 their triangular solves,
-// 32 Z = L^-1 A' and S = Z'Z, 64 the residuals' G pass
+// 32 Z = L^-1 A' and S = Z'Z, 64 the residuals' G pass, 128 compute_scaling,
+// 256 the solves' head (iprod / scale / k2 / W^-1 W^-1)
 #ifndef SOCP_LREP
 #define SOCP_LREP 0
 #endif
@@ -2456,7 +2457,8 @@ struct Large {
       residuals(nd, np_, gap);
       LSTAMP(SP_RESID);
       if (it >= a.maxit) break;
-      const bool dm_it = scaling_op(ll, dm_aa, true);
+      bool dm_it = false;
+      for (int rep = 0; rep < LREP(128); ++rep) dm_it = scaling_op(ll, dm_aa, true);
       LSTAMP(SP_SCALING);
       if (dm_it) {
         status = ST_DOMAIN;
@@ -2479,7 +2481,7 @@ struct Large {
         break;
       }
       LSTAMP(SP_OTHER);
-      solve_head();  // affine direction (solver.jl:125-130)
+      for (int rep = 0; rep < LREP(256); ++rep) solve_head();  // affine direction (solver.jl:125-130)
       LSTAMP(SP_VOP);
       solve_matrix_part(false);
       LSTAMP(SP_SOLVE);
@@ -2492,7 +2494,7 @@ struct Large {
       }
       affine_post(t, ll);
       LSTAMP(SP_STEP);
-      solve_head();  // combined direction (solver.jl:141-145)
+      for (int rep = 0; rep < LREP(256); ++rep) solve_head();  // combined direction (solver.jl:141-145)
       LSTAMP(SP_VOP);
       solve_matrix_part(false);
       LSTAMP(SP_SOLVE);
