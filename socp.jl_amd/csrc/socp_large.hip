@@ -46,6 +46,12 @@
 #ifndef SOCP_LG_SYRK_UNROLL
 #define SOCP_LG_SYRK_UNROLL 1  // blk_gemm's k loop (16 rows per step)
 #endif
+#ifndef SOCP_LG_GRAM_UNROLL
+#define SOCP_LG_GRAM_UNROLL 1  // gram_blkT's 16-row steps per unrolled round
+#endif
+#ifndef SOCP_LG_CATCH_SPLIT_K
+#define SOCP_LG_CATCH_SPLIT_K 2  // split when at most NW / K blocks are left
+#endif
 #ifndef SOCP_LG_ZU
 #define SOCP_LG_ZU 8  // Z = L^-1 A' update: 4-row k-steps per batch of loads (P0 is a multiple of 64; 16: the same time)
 #endif
@@ -715,7 +721,7 @@ struct Large {
   template <bool LO = false, bool FV = true>
   __device__ __forceinline__ void gram_blkT(d4 (&acc)[4][4], gcdbl* Y, int ld, int I0, int J0, gcdbl* fv) {
     const int g = lane >> 4, cl = lane & 15;
-#pragma unroll 1
+#pragma unroll SOCP_LG_GRAM_UNROLL
     for (int k0 = 0; k0 < 64; k0 += 16) {
       double av[4][4], bv[4][4];
 #pragma unroll
@@ -1383,7 +1389,7 @@ struct Large {
   template <int nb>
   __device__ bool chol_nb(gdbl* M, int ld) {
     for (int P = 0; P < nb; ++P) {
-      if (P > 0 && SOCP_LG_CATCH_SPLIT && 2 * (nb - P) <= NW) {
+      if (P > 0 && SOCP_LG_CATCH_SPLIT && SOCP_LG_CATCH_SPLIT_K * (nb - P) <= NW) {
         // few blocks left: each block's catch-up split into its four 16-column
         // groups, one per wavefront (bitwise the whole-block result)
         for (int it = wv; it < 4 * (nb - P); it += NW) {

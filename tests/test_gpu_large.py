@@ -183,6 +183,10 @@ WIDE_N = [
     # (the reference order's dense k^3 iW*iW' takes the oracle ~20 s here: kernel order only)
     dict(n=1100, m=64, k=1200, cones=[(1, 150 * i, 150) for i in range(8)], seed=0x534F4350 + 14, B=1, K=(1,),
          ref=False),
+    # the largest n the blocked kernel takes (NPAD = 2048, 32 tile columns per window: one full window plus
+    # three; the kernel-order oracle takes ~20 s here)
+    dict(n=2048, m=64, k=2100, cones=[(1, 150 * i, 150) for i in range(14)], seed=0x534F4350 + 16, B=1, K=(1,),
+         ref=False),
 ]
 
 
