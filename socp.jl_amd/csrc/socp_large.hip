@@ -858,7 +858,11 @@ struct Large {
   // a wavefront takes FX_CG columns at a time and loads them whole (one HBM
   // round trip per pass), reduces every cone's wbar-weighted tail sum from
   // registers, and writes the columns of X.  Otherwise form_X.
-  static constexpr int FX_CG = 4, FX_NC = 8, FX_R = 10;
+#ifndef SOCP_LG_FX_CG
+#define SOCP_LG_FX_CG 4  // W^-1 G fast path: columns per wavefront pass (2: +2.4 ms at C4, round 5)
+#endif
+  static constexpr int FX_CG = SOCP_LG_FX_CG, FX_NC = 8, FX_R = 10;
+  static_assert(FX_CG * FX_NC <= 32, "per-wavefront fx slots: 32 sums, then 32 head values");
   __device__ bool form_X_fast_ok() const { return nc - csoc <= FX_NC && (k + 63) / 64 <= FX_R; }
   // chunked: X in 4-row chunks, chunk-major -- X[i][j] at ((i/4) NPAD + j) 4 + i%4
   // -- so a chunk is one contiguous 32 NPAD-byte run (the staged SYRK's DMA)

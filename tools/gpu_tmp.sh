@@ -1,8 +1,7 @@
 set -e
 export TMPDIR=/tmp
-O=gpurun_out/final
+O=gpurun_out/cg
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { grep -E "FAILED|ERROR" $O/pytest_gpu.log | head; tail -5 $O/pytest_gpu.log; exit 1; }
-tail -1 $O/pytest_gpu.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
-tail -1 $O/smoke.log
+L="socp.jl_amd/lib/libsocp.so socp.jl_amd/lib/v_lrep0cg2/libsocp.so socp.jl_amd/lib/v_lrep0cg8/libsocp.so"
+timeout -k 10 400 python3 tools/ab_multi.py C4 3 $L $L > $O/ab.log 2>&1 || { tail -30 $O/ab.log; exit 1; }
+grep "^C4" $O/ab.log
