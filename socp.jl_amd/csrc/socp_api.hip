@@ -1000,7 +1000,12 @@ static int sqr_launch(socp_sqr* h, const SqrArgs& a, bool setup, bool timed = tr
   void* kargs[] = {&la};
   if (timed) HIPCHK(timing_begin(ctx));
   const int nt = sqr_block_threads(a.n, a.m);
-  HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(nt), kargs, h->lds, ctx->stream));
+  size_t lds = h->lds;
+  if (!setup && nt == 64) {  // the wave solve kernel's own layout (sqr_solve_layout)
+    const SqrLayout Ls = sqr_solve_layout(a.n, a.m, a.k, a.nc);
+    if (!Ls.large) lds = (size_t)Ls.total * sizeof(double);
+  }
+  HIPCHK(hipLaunchKernel(kern, dim3((unsigned)a.B), dim3(nt), kargs, lds, ctx->stream));
   if (timed) HIPCHK(timing_end(ctx));
   ctx->last_name = nt > 64 ? (setup ? "socp_sqr_setup_wg_kernel" : "socp_sqr_solve_wg_kernel")
                            : (setup ? "socp_sqr_setup_kernel" : "socp_sqr_solve_kernel");

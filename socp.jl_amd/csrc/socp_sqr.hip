@@ -1183,9 +1183,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC >= 64 ? 2
 }
 
 template <int NC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC >= 64 ? 2 : 3))) void socp_sqr_solve_kernel(SqrArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC >= 64 ? SQR_SOLVE_WPE : 3))) void socp_sqr_solve_kernel(SqrArgs a) {
   extern __shared__ double lds_dyn[];
-  const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
+  const SqrLayout L = sqr_solve_layout(a.n, a.m, a.k, a.nc);
   Ctx C{a, L, lds_dyn, (int)threadIdx.x};
   solve_problem<NC>(C, (int64_t)blockIdx.x);
 }

@@ -139,6 +139,23 @@ struct SqrIpmArgs {
   double tol, step, init_eps;
 };
 size_t sqr_ipm_lds_bytes(int n, int m, int k);
+// The wavefront solve kernel reads no H-product chunk buffers: with
+// SQR_SOLVE_TRIM its S block starts where they would (o_X), so its LDS is
+// that much smaller (C2 shape: 19.9 -> 11.2 KB) and more waves fit a CU
+#ifndef SQR_SOLVE_TRIM
+#define SQR_SOLVE_TRIM 1
+#endif
+#ifndef SQR_SOLVE_WPE
+#define SQR_SOLVE_WPE 3  // waves per SIMD the n = 64 solve kernel's registers allow (2: +7 % solve time)
+#endif
+__host__ __device__ inline SqrLayout sqr_solve_layout(int n, int m, int k, int nc) {
+  SqrLayout L = sqr_layout(n, m, k, nc);
+  if (SQR_SOLVE_TRIM && !L.large) {
+    L.o_S = L.o_X;
+    L.total = L.o_S + (m * L.ldm + 3) / 4 * 4;
+  }
+  return L;
+}
 // 0 init, 1 shift, 2 resid, 3 step1, 4 step2 (extra int argument: the iteration), 5 final
 const void* sqr_ipm_kernel_ptr(int which);
 
