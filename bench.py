@@ -16,7 +16,9 @@ Output: one JSON line on rank 0 (driver contract), including
   cpu_baseline — the CPU oracle (reference op order, oracle/) on a bounded
                  sample of the same problems on this host's cores.
 Launch: python bench.py [--gpus N --steps K --warmup W]
-        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+        N>1 with no launcher: bench.py starts the N ranks itself under
+        torch.distributed.run (from a parent that never touches the GPU);
+        under a launcher (WORLD_SIZE set) WORLD_SIZE must equal N.
 """
 from __future__ import annotations
 
@@ -390,7 +392,43 @@ def sqr_bench(args, emit=True):
     return line
 
 
-def main():
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` (N > 1) with no launcher around us: start the N ranks here,
+    one process per GPU under torch.distributed.run (the driver's own launch
+    line), and return its exit code.  This parent never initialises the GPU
+    (no HIP call, no torch.cuda query), so the children start clean."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def stub_shard_solver(B, K, step_s):
+    """--stub-solve (CPU tests of the launcher and the N > 1 accounting only):
+    every problem of the shard 'runs' K iterations and converges, after
+    `step_s` seconds of wall time.  No GPU, no oracle: bench.py's product line
+    is never produced this way on a GPU box (the line names the stub)."""
+    import torch
+
+    def solve():
+        time.sleep(step_s)
+        return {"status": torch.zeros(B, dtype=torch.int32), "iters": torch.full((B,), K, dtype=torch.int32),
+                "res": torch.zeros((B, 3), dtype=torch.float64)}
+    return solve
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -412,23 +450,45 @@ def main():
                          "other-mode summaries (explicit inverse, rank-update plugin): only the timed solver launches")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default: the newest profiles/rNN_pmc_traffic[_<config>].json")
-    args = ap.parse_args()
-    if args.mode == "sqr":
-        return sqr_bench(args)
+    ap.add_argument("--stub-solve", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args(argv)
+    argv = sys.argv[1:] if argv is None else list(argv)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        if args.mode == "sqr":
+            ap.error("--mode sqr is a one-GPU line (the rank-update plugin); run it with --gpus 1")
+        return launch_ranks(args.gpus, argv)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: the launcher and the flag disagree",
+              file=sys.stderr, flush=True)
+        return 2
+    if args.mode == "sqr":
+        if world > 1:
+            print("bench.py: --mode sqr runs on one GPU", file=sys.stderr, flush=True)
+            return 2
+        sqr_bench(args)
+        return 0
+    return run_rank(args, world)
+
+
+def run_rank(args, world):
     import torch
     import torch.distributed as dist
-    import socp_amd as S
     from socp_amd.configs import CONFIGS
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    stub = args.stub_solve
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        if stub:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     cfg = CONFIGS["C2" if args.config == "C3" else args.config]
     B = args.batch or cfg.batch
@@ -436,28 +496,40 @@ def main():
     K = 40 if ref_rule else (args.fixed_k or cfg.fixed_k)  # solver.jl:105
     tol = 1e-5 if ref_rule else 0.0  # solver.jl:122
     n, m, k = cfg.n, cfg.m, cfg.k
-    ctx = S.Context(local)
-    c, A, b, G, h = S.generate(cfg.cones, B, n, m, k, cfg.seed, first_problem=rank * B, ctx=ctx)
-    sing = torch.zeros(B, dtype=torch.uint8, device=dev)  # uniform G (k > n) has full column rank
-    ctx.sync()
     from socp_amd.dist import timed_shard_steps
-    prev = {"out": None}
 
-    def solve_shard():
-        # no host synchronisation inside a step: each launch records its own
-        # HIP event pair on the solver's stream, read after the timed region
-        prev["out"] = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=tol, ctx=ctx,
-                                    out=prev["out"], res=world > 1, explicit_inverse=args.explicit_inverse)
-        return prev["out"]
-
-    def sync():
+    if stub:
+        solve_shard = stub_shard_solver(B, K, 0.01)
+        tr = timed_shard_steps(solve_shard, args.steps, args.warmup)
+        kernel_ms = tr["step_ms"]
+        kname = "stub (--stub-solve: no solver ran)"
+        S = ctx = None
+    else:
+        import socp_amd as S
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        ctx = S.Context(local)
+        c, A, b, G, h = S.generate(cfg.cones, B, n, m, k, cfg.seed, first_problem=rank * B, ctx=ctx)
+        sing = torch.zeros(B, dtype=torch.uint8, device=dev)  # uniform G (k > n) has full column rank
         ctx.sync()
-        torch.cuda.synchronize()
+        prev = {"out": None}
 
-    # warm-up, the K timed steps between barriers, max-over-ranks time, summed
-    # iterations, and (N > 1) the per-step outcome all-gather: socp_amd.dist
-    tr = timed_shard_steps(solve_shard, args.steps, args.warmup, sync=sync)
-    kernel_ms = ctx.kernel_times(args.steps)  # the timed steps' solver launches (the last 64 at most)
+        def solve_shard():
+            # no host synchronisation inside a step: each launch records its own
+            # HIP event pair on the solver's stream, read after the timed region
+            prev["out"] = S.batch_solve(cfg.cones, n, m, k, c, A, b, G, h, sing, maxit=K, tol=tol, ctx=ctx,
+                                        out=prev["out"], res=world > 1, explicit_inverse=args.explicit_inverse)
+            return prev["out"]
+
+        def sync():
+            ctx.sync()
+            torch.cuda.synchronize()
+
+        # warm-up, the K timed steps between barriers, max-over-ranks time, summed
+        # iterations, and (N > 1) the per-step outcome all-gather: socp_amd.dist
+        tr = timed_shard_steps(solve_shard, args.steps, args.warmup, sync=sync)
+        kernel_ms = ctx.kernel_times(args.steps)  # the timed steps' solver launches (the last 64 at most)
+        kname = ctx.last_kernel_name()
     out, dt, iters_total = tr["out"], tr["dt"], tr["iters_total"]
     status_counts = torch.bincount(out["status"].long(), minlength=5).tolist()
 
@@ -465,7 +537,6 @@ def main():
         kms = sum(kernel_ms) / len(kernel_ms)
         iters_per_launch = int(out["iters"].sum().item())
         F = flops_per_problem_iter(n, m, k)
-        kname = ctx.last_kernel_name()
         Fx = (F if args.explicit_inverse else
               flops_executed_per_problem_iter(n, m, k, large="large" in kname))
         Bq = bytes_per_problem_iter(n, m, k)
@@ -478,7 +549,7 @@ def main():
             achieved, peak, unit = F * iters_per_launch / (kms * 1e-3) / 1e12, FP64_PEAK_TFLOPS, "TFLOP/s"
         traffic = None
         tj_path = args.traffic_json or latest_traffic_json(cfg.name)
-        if os.path.exists(tj_path):
+        if os.path.exists(tj_path) and not stub:
             try:
                 tj = json.load(open(tj_path))
                 if tj.get("config") == cfg.name and tj.get("batch") == B and tj.get("fixed_k") == K:
@@ -498,14 +569,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (device SplitMix64 generator, SURVEY.md §8(d); feasible by construction)",
+            "data": ("stub: no solve ran (launcher / accounting test)" if stub else
+                     "synthetic (device SplitMix64 generator, SURVEY.md §8(d); feasible by construction)"),
             "config": {
                 "workload": f"{cfg.name}: {B} problems per GPU, n={n}, m={m}, k={k}, cones {cone_str(cfg.cones)}, "
                             + (f"initial point + reference stopping rule (tol=1e-5 abs, maxit={K}; "
                                f"value counts executed iterations)" if ref_rule else
                                f"initial point + fixed-K={K} IPM iterations (tol=0)")
                             + ("; explicit inverse Li = H^-1 (SOCP_F_EXPLICIT_INVERSE, the reference's "
-                               "op order, densesolver.jl:48)" if args.explicit_inverse else ""),
+                               "op order, densesolver.jl:47-48: potrf, then potrs against I)"
+                               if args.explicit_inverse else ""),
                 "operation_order": "explicit_inverse" if args.explicit_inverse else "cholesky",
                 "global_batch": B * world,
                 "parallelism": f"dp{world} (disjoint problem shards, status all-gather only)",
@@ -532,9 +605,10 @@ def main():
                 "problem_iters_per_launch": iters_per_launch,
             },
         }
-        if world == 1 and not args.no_ingest:
+        extras = world == 1 and not stub
+        if extras and not args.no_ingest:
             line["ingest"] = ingest_line(S, cfg, B, K, tol, (c, A, b, G, h), args.steps, ctx)
-        if world == 1 and not args.explicit_inverse and not ref_rule and not args.no_ingest:
+        if extras and not args.explicit_inverse and not ref_rule and not args.no_ingest:
             # the other operation order on the same batch (never `value`): the
             # reference's explicit Li = H^-1 (SOCP_F_EXPLICIT_INVERSE); its own
             # line is `--explicit-inverse`
@@ -550,9 +624,10 @@ def main():
                 "kernel": ctx.last_kernel_name(), "kernel_ms": xi_kms,
                 "value_kernel": xi_it / (xi_kms * 1e-3), "unit": "problem-iterations/s (solver kernel time)",
                 "frac": F * xi_it / (xi_kms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                "mode": "bench.py --explicit-inverse: Li = H^-1 formed by the Gauss-Jordan sweep (densesolver.jl:48), "
-                        "frac by the SURVEY.md §8(d) formula (which this order executes)"}
-        if world == 1 and not args.no_ingest and cfg.name == "C2" and not ref_rule:
+                "mode": "bench.py --explicit-inverse: Li = H^-1 formed from the Cholesky factor as "
+                        "densesolver.jl:47-48 forms it (potrf, then triangular solves against I); frac by the "
+                        "SURVEY.md §8(d) formula (which this order executes)"}
+        if extras and not args.no_ingest and cfg.name == "C2" and not ref_rule:
             # the rank-update plugin (SparseSolver + SqrScaling, socp_sqr_*) at the same shape: its
             # own line is `--mode sqr`; summarised here so every default run records it
             sq = sqr_bench(argparse.Namespace(config=cfg.name, batch=B, steps=args.steps, warmup=1, no_cpu=True,
@@ -561,7 +636,7 @@ def main():
                                           "kernels_ms": sq["kernels"], "status_counts": sq["status_counts"],
                                           "solve_socp": sq["solve_socp"],
                                           "mode": "bench.py --mode sqr (setup_iter + 2 x solve_kkt per problem)"}
-        if not args.no_cpu and world == 1:  # the CPU leg: rank 0 at N=1 only
+        if not args.no_cpu and extras:  # the CPU leg: rank 0 at N=1 only
             line["cpu_baseline"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol)
             line["cpu_baseline_structured"] = cpu_baseline(cfg, K, budget_s=args.cpu_seconds, tol=tol,
                                                            structured=True)
@@ -573,7 +648,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -199,9 +199,11 @@ extern "C" int socp_kernel_times(socp_ctx* c, float* ms, int n) {
   int64_t cnt = c->tlaunches < n ? c->tlaunches : n;
   if (cnt > socp_ctx::NTIME) cnt = socp_ctx::NTIME;
   if (cnt == 0) return 0;
-  HIPCHK(hipEventSynchronize(c->tev1[(c->tlaunches - 1) % socp_ctx::NTIME]));
   for (int64_t j = 0; j < cnt; ++j) {
     const int i = (int)((c->tlaunches - cnt + j) % socp_ctx::NTIME);
+    // each pair is waited on: the pairs may lie on different streams when the
+    // context's stream was switched inside the window (socp_ctx_set_stream)
+    HIPCHK(hipEventSynchronize(c->tev1[i]));
     HIPCHK(hipEventElapsedTime(&ms[j], c->tev0[i], c->tev1[i]));
   }
   c->last_ms = ms[cnt - 1];
@@ -1146,6 +1148,12 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
   sv.dx = ia.dx; sv.dy = ia.dy; sv.dz = ia.dz; sv.ds = ia.ds;
   sv.cx = ia.rx; sv.cy = ia.ry; sv.cz = ia.rz; sv.cs = ia.rs; sv.status = st_solve; sv.active = nullptr;
   const size_t lds = sqr_ipm_lds_bytes(n, m, k);
+  if (lds > 64 * 1024) {
+    // above the default 64 KiB of dynamic LDS every IPM kernel has to opt in,
+    // as sqr_create does for the setup / solve kernels
+    for (int which = 0; which < 6; ++which)
+      HIPCHK(hipFuncSetAttribute(sqr_ipm_kernel_ptr(which), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  }
   const dim3 grid((unsigned)B), blk(64);
   auto ipm = [&](int which, int it) -> int {
     void* args1[] = {&ia};

@@ -237,3 +237,76 @@ def test_abi_outcome_gather_fresh_context_converted_inputs():
             assert torch.equal(out[0, :, 0], st.to(torch.int32)) and torch.equal(out[0, :, 1], it.to(torch.int32))
     finally:
         comm.close()
+
+
+def _bench_env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env["CUDA_VISIBLE_DEVICES"] = ""  # the stub ranks never touch a GPU
+    env["OMP_NUM_THREADS"] = "1"
+    return env
+
+
+def _bench_json(stdout):
+    import json
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_bench_launcher_starts_n_ranks():
+    """`python bench.py --gpus 2` with no launcher starts two ranks itself
+    (torch.distributed.run from a parent that never touches the GPU); rank 0
+    prints one line for the whole job: n_gpus 2, global batch 2 B, the
+    iterations of both shards over the max-over-ranks time.  The shard solve
+    is bench.py's --stub-solve (gloo, K iterations per problem, no GPU)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    B, steps, K = 96, 3, 8
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", str(steps),
+                        "--warmup", "1", "--batch", str(B), "--stub-solve"],
+                       capture_output=True, text=True, timeout=300, env=_bench_env(), cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _bench_json(r.stdout)
+    assert line["n_gpus"] == 2
+    assert line["config"]["global_batch"] == 2 * B
+    assert line["config"]["parallelism"].startswith("dp2")
+    assert line["steps"] == steps and line["warmup"] == 1
+    # value = every rank's problem-iterations / the max-over-ranks time of the timed steps
+    dt = line["ms_per_step"] * steps / 1e3
+    assert abs(line["value"] * dt - 2 * B * K * steps) <= 1e-6 * 2 * B * K * steps
+    assert line["ms_per_step"] >= 10.0  # the stub's 10 ms per step
+    assert line["cpu_baseline"] is None  # the CPU leg runs at N=1 only
+
+
+def test_bench_one_gpu_line_unchanged_shape():
+    """--gpus 1 stays one process: n_gpus 1, global batch B."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--batch", "32", "--stub-solve", "--no-cpu"],
+                       capture_output=True, text=True, timeout=300, env=_bench_env(), cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _bench_json(r.stdout)
+    assert line["n_gpus"] == 1 and line["config"]["global_batch"] == 32
+    assert line["config"]["parallelism"].startswith("dp1")
+
+
+def test_bench_world_size_mismatch_fails():
+    """Under a launcher, WORLD_SIZE must equal --gpus: a mismatch exits non-zero
+    before any process group or device is touched."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = _bench_env()
+    env.update(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--stub-solve"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=3" in r.stderr
+    env.update(WORLD_SIZE="2")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--stub-solve"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert r.returncode != 0

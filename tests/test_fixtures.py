@@ -133,3 +133,31 @@ def test_c2_trajectory_through_bench_k(fixture, oracle):
                 worst.append((e / tol, K, p, key, e, tol))
                 assert e <= tol, (K, p, key, e, tol)
     print("worst error/tolerance ratios:", sorted(worst, reverse=True)[:3])
+
+
+def test_oracle_reproduces_chaos_floor(oracle):
+    """The committed chaos floor (tests/golden/c2_chaos_floor.json, the outcome
+    gates' rule) is what make_chaos_floor.py computes: one of its
+    comparisons -- the Cholesky-order oracle against itself with G perturbed by
+    one ulp (seed 1) -- recomputed here and equal to the committed row."""
+    import sys
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    import make_chaos_floor as M
+    from socp_amd.configs import C2
+    with open(os.path.join(HERE, "golden", "c2_chaos_floor.json")) as f:
+        fl = json.load(f)
+    assert fl["batch"] == M.B and fl["seeds"] == list(M.SEEDS) and fl["seed"] == C2.seed
+    cfg = C2
+    d = oracle.generate(cfg.cones, M.B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    P = oracle.Params(maxit=40, tol=1e-5, flags=oracle.F_STRUCTURED | oracle.F_CHOLSOLVE)
+    runs = []
+    for seed in (0, 1):
+        G = d["G"] if seed == 0 else M.perturb_G(d["G"], seed)
+        r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], G, d["h"],
+                               sing=np.zeros(M.B, np.uint8), params=P, nthreads=os.cpu_count())
+        runs.append({"status": r["status"], "iters": r["iters"]})
+        assert np.bincount(r["status"], minlength=5).tolist() == fl["histograms"][f"structured_chol/{seed}"]
+    row = M.stats(runs[1], runs[0], symmetric=True)
+    want = fl["self"]["structured_chol"]["per_seed"][0]
+    for key, v in row.items():
+        assert v == pytest.approx(want[key], abs=1e-12), key

@@ -157,22 +157,36 @@ def test_teacher_forced_one_step(oracle, cfg):
 
 @pytest.mark.parametrize("cfg,B", [(C1, 256), (C2, 256)])
 def test_outcome_parity(oracle, cfg, B):
-    """P5 on problems where the oracle converges.  Late iterations are chaotic
-    (SURVEY.md §0.7): the reference formulation jams near tol=1e-5 on part of C2,
-    so the iteration-count gate is asserted on >= 90% of them at C2 and on all at C1."""
+    """P5 on problems where the oracle (reference order) converges.  Late
+    iterations are chaotic.  C1: every oracle-converged problem
+    converges on the GPU within one iteration.  C2: the gates are the chaos
+    floor of the same comparison done on the CPU -- the oracle in the kernels'
+    order (F_STRUCTURED | F_CHOLSOLVE, unperturbed and G perturbed by one ulp)
+    against the reference-order oracle on these 256 problems
+    (tests/golden/c2_chaos_floor.json, "cross/first256") -- minus one point and
+    one problem's share (the rule of test_gpu_outcomes.py)."""
     d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
     r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"])
     g = gpu_batch(dims(cfg), d, B, res=True)
     ok = r["status"] == 0
     assert ok.sum() >= (0.3 * B if cfg is C2 else 0.95 * B)
     gok = g["status"] == 0
-    # C2: a few oracle-converged problems jam for ~20 iterations in the reference
-    # before converging late (tools/c2_outcome.py); the device may end those differently
-    assert gok[ok].mean() >= (0.95 if cfg is C2 else 1.0), gok[ok].mean()
     both = ok & gok
     itok = np.abs(g["iters"] - r["iters"]) <= 1
     frac = itok[both].mean()
-    assert frac >= (0.9 if cfg is C2 else 1.0), frac
+    if cfg is C2:
+        import json
+        import os
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2_chaos_floor.json")) as f:
+            fl = json.load(f)
+        assert fl["batch"] >= B and fl["seed"] == cfg.seed
+        floor = fl["cross"]["structured_chol_vs_reference_order/first256"]["floor"]
+        slack = fl["gate_slack"]
+        assert gok[ok].mean() >= floor["of_conv"] - slack - 1.0 / ok.sum(), (gok[ok].mean(), floor)
+        assert frac >= floor["iters1"] - slack - 1.0 / both.sum(), (frac, floor)
+    else:
+        assert gok[ok].all(), gok[ok].mean()
+        assert frac == 1.0, frac
     dx = np.abs(g["x"].reshape(B, -1) - r["x"].reshape(B, -1)).max(axis=1)
     assert dx[both].max() <= 1e-3
     # everything the GPU reports as converged meets the reference exit test

@@ -12,7 +12,8 @@ dense factor, so agreement is to rounding, never bitwise):
     rank-update restatement, rel <= 1e-9 where kappa(H) <= 1e5; HIP sqr vs the
     HIP dense plugin at the same tolerance; m = 0 and sing problems;
   * every instantiation (NC = 16, 32, 48, 64) and the shape limits (m = 64,
-    k = 256, 15 cones, an LP with no SOC cone) vs the oracle, gate
+    15 cones, k = 1000 on one wavefront, n = 1000 / m = 300 on the workgroup
+    kernels, an LP with no SOC cone) vs the oracle, gate
     max(1e-9, 1e-15 kappa(H) kappa(S));
   * failures (domain error, lost definiteness in a downdate) stay in their
     problem; solve_kkt before setup_iter is refused; per-call H2D bytes.
@@ -242,7 +243,8 @@ def _interior(rng, cones, B, k):
     (17, 3, 25, [(1, 0, 5), (1, 5, 9), (1, 14, 11)]),            # NC = 32, ragged, three SOC cones
     (64, 64, 100, [(0, 0, 36), (1, 36, 64)]),                    # m at its limit, k > 64
     (9, 0, 12, [(0, 0, 12)]),                                    # LP: no SOC cone, no modification
-    (30, 5, 256, [(0, 0, 16)] + [(1, 16 + 16 * i, 16) for i in range(15)]),  # k at its limit, 15 cones
+    (30, 5, 256, [(0, 0, 16)] + [(1, 16 + 16 * i, 16) for i in range(15)]),  # 15 cones
+    (30, 5, 1000, [(0, 0, 100)] + [(1, 100 + 75 * i, 75) for i in range(12)]),  # one wavefront, k > 256
 ])
 def test_sqr_shapes_vs_oracle(oracle, n, m, k, cones):
     rng = np.random.default_rng(n * 1000 + m * 10 + k)
@@ -318,6 +320,9 @@ def test_sqr_optimal_control_n150(oracle):
     (300, 120, 400, [(0, 0, 100)] + [(1, 100 * i, 100) for i in range(1, 4)], False),
     (520, 200, 600, [(1, 0, 300), (1, 300, 300)], False),
     (256, 256, 300, [(1, 0, 150), (1, 150, 150)], True),            # sing, m = n
+    # near the advertised limits (n, m <= 1024): factors and C in the record,
+    # m > 256 (the two-pass residual form's range)
+    (1000, 300, 1100, [(0, 0, 100)] + [(1, 100 + 200 * i, 200) for i in range(5)], False),
 ])
 def test_sqr_workgroup_shapes_vs_oracle(oracle, n, m, k, cones, sing):
     rng = np.random.default_rng(n * 1000 + m * 10 + k)
@@ -364,6 +369,28 @@ def test_sqr_solve_socp_large_shape(oracle):
     B = 2
     d = oracle.generate(cones, B, n, m, k, 0x534F4350 + 21)
     for K in (1, 2):
+        r = oracle.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"], sing=np.zeros(B, np.uint8),
+                               params=oracle.Params(maxit=K, tol=0.0, flags=oracle.F_SQR))
+        hd = S.SqrHandle(cones, n, m, k, d["A"], d["G"], np.zeros(B, np.uint8))
+        g = hd.solve_socp(d["c"], d["b"], d["h"], maxit=K, tol=0.0)
+        assert (g["status"] == r["status"]).all() and (g["iters"] == r["iters"]).all()
+        for p in range(B):
+            for key, L in (("x", n), ("z", k), ("s", k)):
+                a_, b_ = g[key][p * L:(p + 1) * L], r[key][p * L:(p + 1) * L]
+                e = np.linalg.norm(a_ - b_) / np.linalg.norm(b_)
+                assert e <= 1e-8, (K, p, key, e)
+
+
+def test_sqr_solve_socp_wide_k_dynamic_lds(oracle):
+    """solve_socp with k = 1500 on the one-wavefront plugin kernels: the IPM
+    kernels' vectors ((7k + 64) doubles = 84 KB) pass the default 64 KiB of
+    dynamic LDS, so every IPM kernel opts in (hipFuncSetAttribute).  Fixed-K
+    trajectories vs the oracle's F_SQR IPM, rel <= 1e-8."""
+    n, m, k = 40, 10, 1500
+    cones = [(0, 0, 300)] + [(1, 300 + 100 * i, 100) for i in range(12)]
+    B = 3
+    d = oracle.generate(cones, B, n, m, k, 0x534F4350 + 22)
+    for K in (1, 3):
         r = oracle.batch_solve(cones, n, m, k, d["c"], d["A"], d["b"], d["G"], d["h"], sing=np.zeros(B, np.uint8),
                                params=oracle.Params(maxit=K, tol=0.0, flags=oracle.F_SQR))
         hd = S.SqrHandle(cones, n, m, k, d["A"], d["G"], np.zeros(B, np.uint8))
