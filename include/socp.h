@@ -79,8 +79,10 @@ typedef struct socp_params {
 #define SOCP_F_DEVICE_PTRS 1 /* all data pointers are device (HBM) pointers */
 #define SOCP_F_WARM_START 2  /* x,y,z,s hold the starting iterate: skip the init solve (solver.jl:68-104) */
 #define SOCP_F_FORCE_LARGE 4 /* run the blocked kernel even where the register-resident one applies (testing, tuning) */
-/* Form Li = H^-1 explicitly, as densesolver.jl:48 does (ldiv!(Li, fact, I)),
- * and use it in every solve (:73,83) -- the reference's operation order.  By
+/* Form Li = H^-1 explicitly, as densesolver.jl:47-48 does (ldiv!(Li,
+ * cholesky!(H), I): H = L L', then Li = L^-T L^-1 from the factor; S^-1 the
+ * same way), and use it in every solve (:73,83) -- the reference's operation
+ * order.  By
  * default the kernels factor H = L L' (cholesky!, :47) and replace every
  * product with Li by two triangular solves (A Li enters as Z = L^-1 A',
  * S = Z'Z): the same linear algebra in exact arithmetic, far more accurate
@@ -114,8 +116,7 @@ int socp_ctx_reset_stream(socp_ctx* ctx);
 /* 1 if a compiled kernel accepts the dims: the register-resident kernel (one
  * wavefront per problem, <= 8 cones, m <= 64; k <= 128 for n <= 48, k <= 96
  * for 48 < n <= 64: the compiled variant table, socp.jl_amd/csrc/gen_inst.py)
- * or the blocked kernel (n, m <= 2048 -- 512 with SOCP_F_EXPLICIT_INVERSE,
- * whose sweeps hold a panel row in registers --, <= 64 cones, k <= 2^21 -- its
+ * or the blocked kernel (n, m <= 2048, <= 64 cones, k <= 2^21 -- its
  * LDS / vector offsets are 32-bit; one 512-thread workgroup per problem), which
  * also takes every register-kernel shape.  The
  * blocked kernel keeps the problem's vectors in the 160 KiB LDS of a CU when

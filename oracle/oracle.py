@@ -49,6 +49,7 @@ class Params(C.Structure):
 F_WARM_START = 2
 F_STRUCTURED = 16  # oracle-only: the build's structured algorithm (CPU baseline line)
 F_CHOLSOLVE = 64  # oracle-only, with F_STRUCTURED: Li v by triangular solves, S = Z'Z (the register kernel at m <= 16)
+F_INV_YTY = 128  # oracle-only, with F_STRUCTURED: Li = Y'Y, Y = L^-1 (the kernels' explicit inverse; potrs(I) without it)
 F_SQR = 32  # oracle-only: SqrScaling + SparseSolver (spsolver.jl, the rank-update path)
 
 

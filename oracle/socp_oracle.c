@@ -385,9 +385,12 @@ typedef struct {
   int cholsolve;         /* OR_F_CHOLSOLVE (with structured): no explicit Li -- Z = U^-T A' kept in
                             ALi (as Z', m x n), S = Z'Z, Li v by the two triangular solves of potrs
                             (the register kernel's order for m <= 16) */
+  int inv_yty;           /* OR_F_INV_YTY (with structured, without cholsolve): Li = Y'Y with
+                            Y = U^-T = L^-1 formed by forward substitution against I (potri's
+                            order, the kernels' explicit inverse) instead of potrs(I) */
   const cones_t* C;
   const double *A, *G; /* column-major m x n, k x n */
-  double *AA, *GWiWi, *H, *Li, *ALi, *S;
+  double *AA, *GWiWi, *H, *Li, *ALi, *S, *Y;
   double *k0, *k1, *k2, *m0, *n0, *n1;
 } dense_t;
 
@@ -446,6 +449,25 @@ static int setup_iter(dense_t* D, const scaling_t* S) {
     if (potrf_u(D->S, m)) return 3;
     return 0;
   }
+  if (D->inv_yty) {
+    /* Y = U^-T = L^-1 (lower), column j by forward substitution U'y = e_j */
+    double* Y = D->Y;
+    for (int j = 0; j < n; ++j) {
+      double* y = Y + (size_t)j * n;
+      for (int i = 0; i < n; ++i) {
+        double t = (i == j) ? 1.0 : 0.0;
+        for (int q = j; q < i; ++q) t -= M(D->H, n, q, i) * y[q];
+        y[i] = (i < j) ? 0.0 : t / M(D->H, n, i, i);
+      }
+    }
+    /* Li = Y'Y: Li[a][b] = sum_{q >= max(a, b)} Y[q][a] Y[q][b] */
+    for (int b = 0; b < n; ++b)
+      for (int a = 0; a < n; ++a) {
+        double acc = 0.0;
+        for (int q = (a > b ? a : b); q < n; ++q) acc += Y[(size_t)a * n + q] * Y[(size_t)b * n + q];
+        M(D->Li, n, a, b) = acc;
+      }
+  } else
   /* Li = H^-1 via ldiv!(Li, fact, I) */
   for (int j = 0; j < n; ++j) {
     double* col = D->Li + (size_t)j * n;
@@ -827,7 +849,7 @@ static int ws_init(ws_t* w, int n, int m, int k, int ncones, int maxdim) {
   SZ(sizeof(double) * k * 2);
   SZ(sizeof(double) * ncones);
   SZ(sizeof(double) * maxdim * 2);
-  SZ(sizeof(double) * n * n * 3);
+  SZ(sizeof(double) * n * n * 4);
   SZ(sizeof(double) * n * k);
   SZ(sizeof(double) * m * n);
   SZ(sizeof(double) * m * m);
@@ -859,10 +881,12 @@ static int ws_init(ws_t* w, int n, int m, int k, int ncones, int maxdim) {
   w->D.k = k;
   w->D.structured = 0;
   w->D.cholsolve = 0;
+  w->D.inv_yty = 0;
   w->D.C = NULL;
   w->D.AA = carve(&p, sizeof(double) * n * n);
   w->D.H = carve(&p, sizeof(double) * n * n);
   w->D.Li = carve(&p, sizeof(double) * n * n);
+  w->D.Y = carve(&p, sizeof(double) * n * n);
   w->D.GWiWi = carve(&p, sizeof(double) * n * k);
   w->D.ALi = carve(&p, sizeof(double) * m * n);
   w->D.S = carve(&p, sizeof(double) * m * m);
@@ -946,6 +970,7 @@ typedef struct {
 #define OR_F_STRUCTURED 16 /* oracle-only: the build's structured algorithm (CPU baseline) */
 #define OR_F_SQR 32        /* oracle-only: SqrScaling + SparseSolver (spsolver.jl) instead of DenseSolver */
 #define OR_F_CHOLSOLVE 64  /* oracle-only, with OR_F_STRUCTURED: triangular solves instead of the explicit Li */
+#define OR_F_INV_YTY 128   /* oracle-only, with OR_F_STRUCTURED: Li = Y'Y, Y = L^-1 (the kernels' explicit inverse) */
 
 static double dot(const double* a, const double* b, int n) {
   double s = 0.0;
@@ -1010,6 +1035,7 @@ static void solve_one(ws_t* w, const cones_t* C, const double* c, const double* 
   D->C = C;
   D->structured = (P->flags & OR_F_STRUCTURED) != 0;
   D->cholsolve = D->structured && (P->flags & OR_F_CHOLSOLVE) != 0;
+  D->inv_yty = D->structured && !D->cholsolve && (P->flags & OR_F_INV_YTY) != 0;
   const int sqr = (P->flags & OR_F_SQR) != 0;
 #define KKT(a, b_, c_, d, e, f, g, h_) \
   (sqr ? sqr_solve_kkt(D, C, S, a, b_, c_, d, e, f, g, h_) : solve_kkt(D, C, S, a, b_, c_, d, e, f, g, h_))
@@ -1228,6 +1254,7 @@ EXPORT int or_kkt_single(int nc, const int32_t* kind, const int32_t* offs, const
   w.D.C = &C;
   w.D.structured = structured != 0; /* the kernels' order (F_STRUCTURED); H output: reference order only */
   w.D.cholsolve = (structured & 2) != 0; /* 2 | 1: with the triangular solves (OR_F_CHOLSOLVE) */
+  w.D.inv_yty = (structured & 1) && !(structured & 2) && (structured & 4); /* 4 | 1: Li = Y'Y (OR_F_INV_YTY) */
   if (structured) Hout = NULL;
   if (structured & 2) Liout = NULL;
   for (int bq = 0; bq < n; ++bq)

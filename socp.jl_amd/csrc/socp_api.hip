@@ -260,8 +260,7 @@ static const SmallVariant* pick_variant(int n, int m, int k) {
   return best;
 }
 
-// The blocked kernel (socp_large.hip): n, m <= 512 (a swept panel row is held
-// in registers).  The problem's vectors live in the 160 KiB LDS of a CU when
+// The blocked kernel (socp_large.hip): n, m <= 2048.  The problem's vectors live in the 160 KiB LDS of a CU when
 // they fit; otherwise (e.g. k = 1000 at n = 512) in the workgroup's slot of the
 // HBM workspace (*gv: the GV kernels), with only the problem index in LDS.
 static bool large_fits(int n, int m, int k, int nc, size_t* lds_bytes, bool* gv = nullptr, bool xi = false) {
@@ -278,11 +277,10 @@ static bool large_fits(int n, int m, int k, int nc, size_t* lds_bytes, bool* gv 
   }
   const LargeLayout L = large_layout(n, m, k);
   // n, m: up to 64 LARGE_NB_MAX_CHOL with Cholesky factors of H and S (wide
-  // panels in windows, socp_large.hip panel_chol_wide; S is swept up to 512),
-  // 64 LARGE_NB_MAX where H and S are swept (SOCP_F_EXPLICIT_INVERSE: a panel
-  // row in registers)
-  const int nb_max = xi ? LARGE_NB_MAX : LARGE_NB_MAX_CHOL;
-  if (L.NPAD > 64 * nb_max || L.MPAD > 64 * nb_max || nc > MAXC) return false;
+  // panels in windows, socp_large.hip panel_chol_wide), in both operation
+  // orders (SOCP_F_EXPLICIT_INVERSE forms Li and S^-1 from those factors)
+  (void)xi;
+  if (L.NPAD > 64 * LARGE_NB_MAX_CHOL || L.MPAD > 64 * LARGE_NB_MAX_CHOL || nc > MAXC) return false;
   size_t lds = (size_t)L.total * sizeof(double);
   const bool g = lds + 64 > 160 * 1024;
   if (g) lds = 64 * sizeof(double);
@@ -299,7 +297,7 @@ extern "C" int socp_supported(const socp_dims* d) {
 
 static const char* kUnsupported =
     "dims outside both kernels (register-resident: n, m <= 64, k <= 128, <= 8 cones; "
-    "blocked: n, m <= 2048 (512 with SOCP_F_EXPLICIT_INVERSE), <= 64 cones, k <= 2^21)";
+    "blocked: n, m <= 2048, <= 64 cones, k <= 2^21)";
 
 // ---------------------------------------------------------------- launch
 static unsigned long long* g_stamps = nullptr;  // per-phase cycle table (SOCP_DIAG builds)

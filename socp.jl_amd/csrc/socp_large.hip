@@ -137,8 +137,11 @@ __device__ __forceinline__ double wave_max(double v) {
 #ifndef SOCP_LG_PANEL
 #define SOCP_LG_PANEL 1  // 0: the per-pivot rank-1 sweep of a panel (A/B builds)
 #endif
+#ifndef SOCP_LG_INV_CHOL
+#define SOCP_LG_INV_CHOL 1  // 0: explicit inverses by the Gauss-Jordan sweep (A/B builds)
+#endif
 #ifndef SOCP_LG_CHOL
-#define SOCP_LG_CHOL 1  // 0: Li = H^-1 by the Gauss-Jordan sweep (A/B builds)
+#define SOCP_LG_CHOL 1  // 0: Li = H^-1 formed (A/B builds)
 #endif
 
 // C += U'V (NEG = 1: C -= U'V) for C/D-layout 16x16 tiles (socp_small.hpp's
@@ -150,12 +153,17 @@ __device__ __forceinline__ d4 tile_mm(const d4& U, const d4& V, d4 C) {
   return C;
 }
 
-// XI (SOCP_F_EXPLICIT_INVERSE): Li = H^-1 by the blocked Gauss-Jordan sweep,
-// the reference's operation order (densesolver.jl:48), instead of H = L L'.
+// XI (SOCP_F_EXPLICIT_INVERSE): Li = H^-1 formed from the Cholesky factor
+// (chol_inverse), the reference's operation order (densesolver.jl:47-48),
+// instead of the triangular solves against H = L L'.
 // GV: the vectors in global memory (LV above).
 template <bool XI, bool GV>
 struct Large {
   static constexpr bool CHOL = SOCP_LG_CHOL && !XI;
+  // where Li = H^-1 is formed (XI, and every shape of a SOCP_LG_CHOL=0 build):
+  // from the Cholesky factor, Li = L^-T L^-1 (chol_inverse), as
+  // densesolver.jl:47-48 forms it; S^-1 likewise (0: the Gauss-Jordan sweep)
+  static constexpr bool INV_CHOL = SOCP_LG_INV_CHOL && !CHOL;
   gdbl* gvec = nullptr;  // GV: this workgroup's vector region (workspace slot)
   __device__ __forceinline__ auto& lvref(int i) const {
     if constexpr (GV)
@@ -1686,6 +1694,103 @@ struct Large {
     BAR();
   }
 
+  // The explicit inverse from the factor chol() leaves in M (column-major, L
+  // below the diagonal blocks, E_P = L_PP^-1 in them): densesolver.jl:47-48,
+  // Li = ldiv!(cholesky!(H), I) = L^-T L^-1.
+  // (1) Y = L^-1 (row-major in Yp, ld x ld) by block forward substitution, one
+  //     64-row panel per step: a wavefront owns a 16-column tile of the panel
+  //     rows, R = -sum_{c0 <= y < P0} L[P rows][y] Y[y][cols] (four 16x16
+  //     accumulators, MFMA, Y lower so the sum starts at the tile's column),
+  //     then Y[P rows][cols] = E_P R; the diagonal block is E_P itself;
+  // (2) M = Y'Y in both triangles (64x64 blocks, the Gram products of the
+  //     panels P >= I of block (I, J), as form_S_gram), symmetric by
+  //     construction.  Padding rows / columns carry the identity through.
+  __device__ void chol_inverse(gdbl* M, int ld) {
+    const int NB = ld / 64;
+    gdbl* const Y = Yp;
+    const d4 zero = {0.0, 0.0, 0.0, 0.0};
+    for (int P = 0; P < NB; ++P) {
+      const int P0 = 64 * P;
+      for (int tb = wv; tb < 4 * P + 4; tb += NW) {
+        LANE_IDS();
+        const int c0 = 16 * tb;
+        d4 out[4];
+        if (tb >= 4 * P) {
+          const int x = c0 - P0 + cl;  // E_P lower: zero above its diagonal
+#pragma unroll
+          for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int i = 16 * ta + g + 4 * r;
+              out[ta][r] = (x <= i) ? M[(int64_t)(P0 + x) * ld + P0 + i] : 0.0;
+            }
+        } else {
+          d4 acc[4] = {zero, zero, zero, zero};
+          for (int y0 = c0; y0 < P0; y0 += 16) {  // 16 rows per round trip
+            double a[4][4], b[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int y = y0 + 4 * u + g;
+              b[u] = Y[(int64_t)y * ld + c0 + cl];
+#pragma unroll
+              for (int ta = 0; ta < 4; ++ta) a[u][ta] = M[(int64_t)y * ld + P0 + 16 * ta + cl];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int ta = 0; ta < 4; ++ta)
+                acc[ta] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][ta], b[u], acc[ta], 0, 0, 1);  // -= L Y
+          }
+#pragma unroll
+          for (int tc = 0; tc < 4; ++tc) {  // out_tc = sum_{ta <= tc} E[tc][ta] R_ta
+            d4 o = zero;
+#pragma unroll
+            for (int ta = 0; ta <= tc; ++ta)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int x = 16 * ta + g + 4 * r, i = 16 * tc + cl;
+                const double ev = (x <= i) ? M[(int64_t)(P0 + x) * ld + P0 + i] : 0.0;
+                o = __builtin_amdgcn_mfma_f64_16x16x4f64(ev, acc[ta][r], o, 0, 0, 0);
+              }
+            out[tc] = o;
+          }
+        }
+#pragma unroll
+        for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Y[(int64_t)(P0 + 16 * ta + g + 4 * r) * ld + c0 + cl] = out[ta][r];
+      }
+      BAR();  // the panel's rows of Y complete before the next panel reads them
+    }
+    for (int t = wv; t < NB * (NB + 1) / 2; t += NW) {
+      LANE_IDS();
+      int I, J;
+      tri_ij(t, I, J);
+      d4 acc[4][4];
+      zero_blk(acc);
+      for (int P = I; P < NB; ++P) {
+        if (I == J)
+          gram_blkT<true, false>(acc, Y + (int64_t)64 * P * ld, ld, 64 * I, 64 * J, nullptr);
+        else
+          gram_blkT<false, false>(acc, Y + (int64_t)64 * P * ld, ld, 64 * I, 64 * J, nullptr);
+      }
+#pragma unroll
+      for (int a_ = 0; a_ < 4; ++a_)
+#pragma unroll
+        for (int b_ = 0; b_ < 4; ++b_)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (I == J && b_ < a_) continue;
+            const int i = 64 * I + 16 * b_ + cl, j = 64 * J + 16 * a_ + g + 4 * r;
+            if (i < j) continue;  // upper half of a diagonal tile: its mirror is written
+            const double v = acc[a_][b_][r];
+            M[(int64_t)j * ld + i] = v;
+            if (i != j) M[(int64_t)i * ld + j] = v;
+          }
+    }
+    BAR();
+  }
+
   // Blocked symmetric Gauss-Jordan sweep of the 64nb x 64nb symmetric matrix
   // whose lower triangle is stored in M (column-major, ld); leaves -M^-1 in the
   // lower triangle.  Panel P: thread (wave w, lane l) holds panel rows
@@ -1918,10 +2023,15 @@ struct Large {
     }
     LSTAMP(SP_SCHUR);
     } else {
-    if (!sweep(Hm, L.NPAD)) return ST_CHOL_H;
-    if (h_only) return 0;
-    LSTAMP(SP_SWEEP_H);
-    finalize_sym(Hm, L.NPAD);
+    if constexpr (INV_CHOL) {
+      if (!chol(Hm, L.NPAD)) return ST_CHOL_H;
+      if (h_only) return 0;
+      chol_inverse(Hm, L.NPAD);
+    } else {
+      if (!sweep(Hm, L.NPAD)) return ST_CHOL_H;
+      if (h_only) return 0;
+      finalize_sym(Hm, L.NPAD);
+    }
     LSTAMP(NSTAMP + 1 + 4);
     LSTAMP(SP_SWEEP_H);
     const int NB = L.NPAD / 64, MB = L.MPAD / 64;
@@ -1952,8 +2062,13 @@ struct Large {
       LSTAMP(SP_SCHUR);
       return 0;
     }
-    if (!sweep(Sm, L.MPAD)) return ST_CHOL_S;
-    finalize_sym(Sm, L.MPAD);
+    if constexpr (INV_CHOL) {
+      if (!chol(Sm, L.MPAD)) return ST_CHOL_S;
+      chol_inverse(Sm, L.MPAD);
+    } else {
+      if (!sweep(Sm, L.MPAD)) return ST_CHOL_S;
+      finalize_sym(Sm, L.MPAD);
+    }
     LSTAMP(SP_SCHUR);
     return 0;
   }

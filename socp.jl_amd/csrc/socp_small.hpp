@@ -762,9 +762,9 @@ __device__ __forceinline__ void factor_tile(d4 Dt, d4& W, bool& ok, const H& hoo
 }
 
 
-// XI (SOCP_F_EXPLICIT_INVERSE): Li = H^-1 by the Gauss-Jordan sweep on every
-// shape -- the reference's operation order (densesolver.jl:48 forms Li
-// explicitly) -- instead of the Cholesky path of the m <= 16 shapes.
+// XI (SOCP_F_EXPLICIT_INVERSE): Li = H^-1 formed on every shape -- the
+// reference's operation order (densesolver.jl:47-48 forms Li = L^-T L^-1 from
+// cholesky!(H)) -- instead of the triangular solves of the m <= 16 shapes.
 template <int NQ, int NP, int MQ, bool XI = false>
 struct Small {
   using SH = Shape<NQ, NP, MQ>;
@@ -824,6 +824,14 @@ struct Small {
   // and its products are triangular solves (trsv_fwd / trsv_bwd).  Larger m
   // keep the explicit inverse by the sweep.
   static constexpr bool CHOL = SOCP_SMALL_CHOL && AL_LDS && !KEEP_AL && !XI;
+#ifndef SOCP_INV_CHOL
+#define SOCP_INV_CHOL 1  // 0: the explicit inverses by the Gauss-Jordan sweep (A/B builds)
+#endif
+  // where Li = H^-1 is formed (XI; the m > 16 shapes): from the Cholesky
+  // factor, Li = L^-T L^-1 (densesolver.jl:47-48, chol_inv), and likewise
+  // S^-1; the SYRK then leaves H in the upper-block form chol() reads
+  static constexpr bool INV_CHOL = SOCP_INV_CHOL && !CHOL;
+  static constexpr bool UPPER_H = CHOL || INV_CHOL;
 
   __device__ __forceinline__ Small(const SmallArgs& args)
       : a(args), lane(threadIdx.x), g(threadIdx.x >> 4), cl(threadIdx.x & 15),
@@ -1781,7 +1789,7 @@ struct Small {
 #pragma unroll
       for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
-        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = CHOL ? mfma(Xc[tj], Xc[ti], T[tri(ti, tj)])
+        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = UPPER_H ? mfma(Xc[tj], Xc[ti], T[tri(ti, tj)])
                                                                 : mfma(Xc[ti], Xc[tj], T[tri(ti, tj)]);
       if (pp + 1 < NP) {
         // the step's LDS reads behind the first MFMAs, its VALU after them
@@ -1813,7 +1821,7 @@ struct Small {
 #pragma unroll
       for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
-        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = CHOL ? mfma(Xc[tj], Xc[ti], T[tri(ti, tj)])   // block (tj, ti)
+        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = UPPER_H ? mfma(Xc[tj], Xc[ti], T[tri(ti, tj)])   // block (tj, ti)
                                                                 : mfma(Xc[ti], Xc[tj], T[tri(ti, tj)]);  // block (ti, tj)
       if (pp + 1 < NP) {
 #pragma unroll
@@ -1835,7 +1843,7 @@ struct Small {
 #pragma unroll
       for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
-        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = CHOL ? mfma(X[tj], X[ti], T[tri(ti, tj)]) : mfma(X[ti], X[tj], T[tri(ti, tj)]);
+        for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = UPPER_H ? mfma(X[tj], X[ti], T[tri(ti, tj)]) : mfma(X[ti], X[tj], T[tri(ti, tj)]);
       if (pp % 2 == 1) SCHED_FENCE();
     }
 #endif
@@ -1851,7 +1859,7 @@ struct Small {
 #pragma unroll
           for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
-            for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = CHOL ? mfma(Aq[tj], Aq[ti], T[tri(ti, tj)]) : mfma(Aq[ti], Aq[tj], T[tri(ti, tj)]);
+            for (int tj = 0; tj <= ti; ++tj) T[tri(ti, tj)] = UPPER_H ? mfma(Aq[tj], Aq[ti], T[tri(ti, tj)]) : mfma(Aq[ti], Aq[tj], T[tri(ti, tj)]);
         }
     }
 #pragma unroll
@@ -2135,6 +2143,114 @@ struct Small {
     return ok;
   }
 
+  // ---------------- the explicit inverse from the Cholesky factor (chol_inv)
+  // densesolver.jl:47-48: Li = H^-1 from cholesky!(H), the reference's
+  // ldiv!(Li, fact, I) -- H = L L', then Li = L^-T L^-1 -- on 16x16 tiles:
+  // (1) H = L L' right-looking by tile panels as chol() does it (its look-ahead:
+  //     the next pivot tile factored with the panel's other MFMA work dealt out
+  //     between its row blocks), leaving M[tri(P, P)] = W_P = L_PP^-1 and
+  //     M[tri(i, P)] = L_iP' (i > P); every pivot is potrf's (status 2 / 3);
+  // (2) Y = L^-1 in place, row by row: Y_PP = W_P,
+  //     Y_ab = -W_a sum_{b <= q < a} L_aq Y_qb (a > b);
+  // (3) Li = Y'Y in place, row by row: Li_ab = sum_{q >= a} Y_qa' Y_qb (a >= b),
+  //     symmetric by construction.
+  // In: M in the upper-block form (M[tri(j, i)] = block (i, j), i <= j, the
+  // SYRK's UPPER_H output); out: the lower tiles of the inverse in the natural
+  // C/D layout (M[tri(a, b)] = block (a, b)), as symv and the record read them.
+  struct GCholOp {
+    int kind, i, j;  // 0: M_iP = W_P M_iP (= L_iP'), 1: M_ij -= L_iP L_jP', -1: none
+  };
+  template <int Q, int P>
+  static constexpr GCholOp gchol_op(int idx) {
+    int cnt = 0;
+    for (int i = P + 2; i < Q; ++i)
+      if (cnt++ == idx) return GCholOp{0, i, 0};
+    for (int j = P + 1; j < Q; ++j)
+      for (int i = P + 1; i <= j; ++i) {
+        if (i == P + 1 && j == P + 1) continue;
+        if (cnt++ == idx) return GCholOp{1, i, j};
+      }
+    return GCholOp{-1, 0, 0};
+  }
+  template <int Q, int P>
+  static constexpr int gchol_op_count() {
+    int c = 0;
+    while (gchol_op<Q, P>(c).kind >= 0) ++c;
+    return c;
+  }
+  template <int Q, int P, int LO, int HI>
+  __device__ __forceinline__ static void gchol_ops(d4 (&M)[Q * (Q + 1) / 2], const d4& WT) {
+    if constexpr (LO < HI) {
+      constexpr GCholOp o = gchol_op<Q, P>(LO);
+      if constexpr (o.kind == 0)
+        M[tri(o.i, P)] = mm<0>(WT, M[tri(o.i, P)], (d4){0.0, 0.0, 0.0, 0.0});
+      else
+        M[tri(o.j, o.i)] = mm<1>(M[tri(o.i, P)], M[tri(o.j, P)], M[tri(o.j, o.i)]);
+      gchol_ops<Q, P, LO + 1, HI>(M, WT);
+    }
+  }
+  template <int Q, int P>
+  struct GCholHook {
+    d4 (&M)[Q * (Q + 1) / 2];
+    const d4& WT;
+    template <int B>
+    __device__ __forceinline__ void run() const {
+      constexpr int N = gchol_op_count<Q, P>();
+      gchol_ops<Q, P, (N * B) / 4, (N * (B + 1)) / 4>(M, WT);
+    }
+  };
+  template <int Q, int P>
+  __device__ __forceinline__ void gchol_panel(d4 (&M)[Q * (Q + 1) / 2], const d4& W, bool& ok) {
+    if constexpr (P < Q) {
+      MARK_BEGIN("chol_inv_panel");
+      if constexpr (P + 1 < Q) {
+        const d4 WT = transpose(W);
+        M[tri(P + 1, P)] = mm<0>(WT, M[tri(P + 1, P)], (d4){0.0, 0.0, 0.0, 0.0});
+        M[tri(P + 1, P + 1)] = mm<1>(M[tri(P + 1, P)], M[tri(P + 1, P)], M[tri(P + 1, P + 1)]);
+        d4 Wn;
+        factor_tile<TILE_INPL>(M[tri(P + 1, P + 1)], Wn, ok, GCholHook<Q, P>{M, WT});
+        M[tri(P, P)] = W;
+        gchol_panel<Q, P + 1>(M, Wn, ok);
+      } else {
+        M[tri(P, P)] = W;
+      }
+    }
+  }
+  template <int Q>
+  __device__ __forceinline__ bool chol_inv(d4 (&M)[Q * (Q + 1) / 2]) {
+    MARK_BEGIN("chol_inv");
+    const d4 z = (d4){0.0, 0.0, 0.0, 0.0};
+    bool ok = true;
+    {
+      d4 W;
+      factor_tile<TILE_INPL>(M[tri(0, 0)], W, ok);
+      gchol_panel<Q, 0>(M, W, ok);
+    }
+    // Y = L^-1: row a reads rows q < a of Y (done) and row a of L from column b up
+#pragma unroll
+    for (int a = 1; a < Q; ++a) {
+      const d4 WTa = transpose(M[tri(a, a)]);
+#pragma unroll
+      for (int b = 0; b < a; ++b) {
+        d4 S = mm<0>(M[tri(a, b)], M[tri(b, b)], z);  // L_ab W_b
+#pragma unroll
+        for (int q = b + 1; q < a; ++q) S = mm<0>(M[tri(a, q)], M[tri(q, b)], S);  // + L_aq Y_qb
+        M[tri(a, b)] = mm<1>(WTa, S, z);  // -W_a S
+      }
+    }
+    // Li = Y'Y: tile (a, b) is the last reader of Y_ab (row-major order)
+#pragma unroll
+    for (int a = 0; a < Q; ++a)
+#pragma unroll
+      for (int b = 0; b <= a; ++b) {
+        d4 acc = z;
+#pragma unroll
+        for (int q = a; q < Q; ++q) acc = mm<0>(M[tri(q, a)], M[tri(q, b)], acc);
+        M[tri(a, b)] = acc;
+      }
+    return ok;
+  }
+
   // the transpose buffer, when it lives in dead k-vectors, is zeroed again at
   // the end of a factorisation: their padding rows [k, KP) are never written
   // by the solves and must read as zero (G'T2 reads them against G's zero rows)
@@ -2158,14 +2274,14 @@ struct Small {
     return o;
   }
 
-  __device__ __forceinline__ void dump_sym(double* out) {
+  __device__ __forceinline__ void dump_sym(double* out, bool upper = false) {
 #pragma unroll
     for (int ti = 0; ti < NQ; ++ti)
 #pragma unroll
       for (int tj = 0; tj <= ti; ++tj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int R = 16 * ti + g + 4 * r, Cc = 16 * tj + cl;
+          const int R = (upper ? 16 * tj : 16 * ti) + g + 4 * r, Cc = (upper ? 16 * ti : 16 * tj) + cl;
           if (R < n && Cc < n) {
             out[R * n + Cc] = T[tri(ti, tj)][r];
             if (ti != tj) out[Cc * n + R] = T[tri(ti, tj)][r];
@@ -2186,7 +2302,7 @@ struct Small {
 #ifdef SOCP_DIAG
     // diagnostic dump per problem: H, H^-1 (n x n each), lam, wbar (k each), Li A' (n x m), S (m x m)
     double* dbg = (a.dbg && a.mode == MODE_KKT) ? a.dbg + dbg_p * (int64_t)(2 * n * n + 2 * k + n * m + m * m) : nullptr;
-    if (dbg && !CHOL) dump_sym(dbg);
+    if (dbg && !CHOL) dump_sym(dbg, UPPER_H);
 #endif
     if constexpr (CHOL) {
       const bool okH = chol();
@@ -2219,14 +2335,21 @@ struct Small {
 #endif
       return 0;
     }
-    const bool okH = sweep<NQ, true>(T);
+    bool okH;
+    if constexpr (INV_CHOL) {
+      okH = chol_inv<NQ>(T);
+    } else {
+      okH = sweep<NQ, true>(T);
+    }
     STAMP(SP_SWEEP_H);
     if (!okH) {
       clear_tb();
       return ST_CHOL_H;
     }
+    if constexpr (!INV_CHOL) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) T[t] = -T[t];
+      for (int t = 0; t < NT; ++t) T[t] = -T[t];  // the sweep leaves -H^-1
+    }
 #ifdef SOCP_DIAG
     if (dbg) {
       dump_sym(dbg + n * n);
@@ -2274,7 +2397,11 @@ struct Small {
 #pragma unroll
         for (int tk = 0; tk < NQ; ++tk)
 #pragma unroll
-          for (int s = 0; s < 4; ++s) acc = mfma(LDS(O_A + (16 * tm + cl) * LDA + 16 * tk + g + 4 * s), ALc[tk][s], acc);
+          for (int s = 0; s < 4; ++s) {
+            const double av = LDS(O_A + (16 * tm + cl) * LDA + 16 * tk + g + 4 * s);
+            // INV_CHOL: block (tq, tm) of S, the upper-block form chol_inv reads
+            acc = INV_CHOL ? mfma(ALc[tk][s], av, acc) : mfma(av, ALc[tk][s], acc);
+          }
         Sv[tri(tm, tq)] = acc;
       }
       if constexpr (KEEP_AL) {
@@ -2304,18 +2431,25 @@ struct Small {
         for (int tq = 0; tq <= tm; ++tq)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int R = 16 * tm + g + 4 * r, Cc = 16 * tq + cl;
-            if (R < m && Cc < m) dS[R * m + Cc] = Sv[tri(tm, tq)][r];
+            const int R = (INV_CHOL ? 16 * tq : 16 * tm) + g + 4 * r, Cc = (INV_CHOL ? 16 * tm : 16 * tq) + cl;
+            if (R < m && Cc < m) dS[R * m + Cc] = dS[Cc * m + R] = Sv[tri(tm, tq)][r];
           }
     }
 #endif
     SYNC();
-    const bool okS = sweep<MQ, false>(Sv);
+    bool okS;
+    if constexpr (INV_CHOL) {
+      okS = chol_inv<MQ>(Sv);
+    } else {
+      okS = sweep<MQ, false>(Sv);
+    }
     clear_tb();  // the sweeps' and A Li's transposes ran in the dead k-vectors (TB_ALIAS)
     STAMP(SP_SCHUR);
     if (!okS) return ST_CHOL_S;
+    if constexpr (!INV_CHOL) {
 #pragma unroll
-    for (int t = 0; t < MT; ++t) Sv[t] = -Sv[t];
+      for (int t = 0; t < MT; ++t) Sv[t] = -Sv[t];
+    }
     return 0;
   }
 

@@ -186,7 +186,7 @@ WIDE_N = [
     # the largest n the blocked kernel takes (NPAD = 2048, 32 tile columns per window: one full window plus
     # three; the kernel-order oracle takes ~20 s here)
     dict(n=2048, m=64, k=2100, cones=[(1, 150 * i, 150) for i in range(14)], seed=0x534F4350 + 16, B=1, K=(1,),
-         ref=False),
+         ref=False, xi=False),
 ]
 
 
@@ -197,8 +197,11 @@ def test_wide_n_blocked_cholesky(oracle, shape):
     panels whose right-hand part (more than 32 tile columns) is transformed in
     windows that replay the panel's four tile steps (panel_chol_wide).  Iterates vs the oracle in the kernel's operation
     order (X = W^-1 G, Cholesky + triangular solves) rel <= 1e-8, and vs the
-    reference's own order at the first iteration; the explicit-inverse order
-    (a swept panel row in registers) stays limited to n <= 512."""
+    reference's own order at the first iteration.  The explicit-inverse order
+    (SOCP_F_EXPLICIT_INVERSE: Li = L^-T L^-1 and S^-1 formed from the same
+    factors, chol_inverse) vs the oracle's structured order (Li by potrs(I))
+    at rel <= 1e-8 as well (the n = 2048 case only in the default order: the
+    oracle's n^3 inverse alone takes it a minute)."""
     from types import SimpleNamespace
     cfg = SimpleNamespace(**shape)
     B = shape["B"]
@@ -214,6 +217,12 @@ def test_wide_n_blocked_cholesky(oracle, shape):
         r = oracle_run(oracle, cfg, d, params=oracle.Params(maxit=1, tol=0.0))
         g = run(cfg, d, maxit=1, tol=0.0)
         assert_trajectory(cfg, g, r, B, 1e-8, "reference order")
+    if shape.get("xi", True):
+        for K in shape["K"]:
+            r = oracle_run(oracle, cfg, d, params=oracle.Params(maxit=K, tol=0.0, flags=oracle.F_STRUCTURED))
+            g = run(cfg, d, maxit=K, tol=0.0, explicit_inverse=True)
+            assert S.default_context().last_kernel_name().startswith("socp_large_xi")
+            assert_trajectory(cfg, g, r, B, 1e-8, ("xi", K))
 
 
 def test_c4_trajectory_k1_to_k5_fixture():

@@ -89,10 +89,10 @@ def test_sing_batch_c0b(oracle):
 
 
 def test_beyond_both_kernels_reports_unsupported():
-    # n > 2048 and, for the explicit-inverse order (a swept panel row in
-    # registers), n > 512: outside the blocked kernel (n = 600 in the default
-    # order solves: tests/test_gpu_large.py::test_wide_n_*)
-    for n, xi in ((2100, False), (600, True)):
+    # n > 2048: outside the blocked kernel in both operation orders (n = 600
+    # solves in both: tests/test_gpu_large.py::test_wide_n_*,
+    # tests/test_gpu_large.py::test_wide_n_blocked_cholesky)
+    for n, xi in ((2100, False), (2100, True)):
         k = n + 1
         with pytest.raises(S.SocpError) as e:
             S.batch_solve([(1, 0, k)], n, 0, k, np.zeros(n), None, None, np.zeros(k * n), np.zeros(k),

@@ -1,10 +1,11 @@
 """SOCP_F_EXPLICIT_INVERSE: the reference's operation order on the Cholesky shapes.
 
-densesolver.jl:48 forms Li = H^-1 explicitly (ldiv!(Li, fact, I)) and uses it
-in every solve (:73,83).  By default the register kernel's m <= 16 shapes
-factor H = L L' and solve triangularly instead; with the flag they run the
-Gauss-Jordan sweep (Li formed, as the reference does) -- KM = 2 / 3
-instantiations, so the default kernels are untouched.  Under the reference
+densesolver.jl:47-48 forms Li = H^-1 explicitly from the Cholesky factor
+(ldiv!(Li, cholesky!(H), I)) and uses it in every solve (:73,83).  By default
+the register kernel's m <= 16 shapes factor H = L L' and solve triangularly
+instead; with the flag they form Li = L^-T L^-1 from the same tile factor
+(chol_inv: Y = L^-1 by block forward substitution, Li = Y'Y), and S^-1 the
+same way -- KM = 2 / 3 instantiations, so the default kernels are untouched.  Under the reference
 stopping rule the two modes differ in OUTCOME on a pure LP:
 with the explicit inverse chol(H) fails near the end of every solve, without
 it every problem converges.  The explicit-inverse GPU run must reproduce the
@@ -66,15 +67,16 @@ def test_lp_reference_rule_matches_reference_order(oracle, force_large):
 @pytest.mark.parametrize("cfg,maxk", [(C1, 3), (C2, 6)])
 def test_explicit_inverse_trajectory(oracle, cfg, maxk):
     """P4 for the explicit-inverse kernel: fixed-K iterates vs the oracle's
-    structured order (X = W^-1 G per cone, H = X'X, explicit inverse -- the
-    sweep kernel's algorithm) rel <= 1e-8, and vs the reference order while the
-    systems are well conditioned (first two iterations) rel <= 1e-8."""
+    structured order (X = W^-1 G per cone, H = X'X, Li by potrs(I) -- the
+    reference's inverse) and its Y'Y form (F_INV_YTY, the kernel's) rel <= 1e-8,
+    and vs the reference order while the systems are well conditioned (first
+    two iterations) rel <= 1e-8."""
     B = 16
     d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
     for K in range(1, maxk + 1):
         g = S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
                           np.zeros(B, np.uint8), maxit=K, tol=0.0, explicit_inverse=True)
-        for flags, kmax in ((oracle.F_STRUCTURED, maxk), (0, 2)):
+        for flags, kmax in ((oracle.F_STRUCTURED, maxk), (oracle.F_STRUCTURED | oracle.F_INV_YTY, maxk), (0, 2)):
             if K > kmax:
                 continue
             r = oracle.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
