@@ -135,6 +135,28 @@ def test_c2_trajectory_through_bench_k(fixture, oracle):
     print("worst error/tolerance ratios:", sorted(worst, reverse=True)[:3])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg_name", ["C1", "C2"])
+def test_trajectory_at_its_rounding_floor(oracle, cfg_name):
+    """C1 / C2 at their bench K against the oracle in the kernel's own
+    operation order (X = W^-1 G per cone, H = L L', triangular solves:
+    F_STRUCTURED | F_CHOLSOLVE), with the gate derived from the oracle's
+    sensitivity to one rounding instead of kappa_2(H): rel <= FLOOR_FACTOR *
+    floor_K + FLOOR_ABS for every K and every vector of 8 problems
+    (tests/problems.py trajectory_at_floor)."""
+    import socp_amd as S
+    from problems import trajectory_at_floor
+    from socp_amd.configs import CONFIGS
+    cfg, B = CONFIGS[cfg_name], 8
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    rows = trajectory_at_floor(
+        oracle, cfg, d, B, cfg.fixed_k, oracle.F_STRUCTURED | oracle.F_CHOLSOLVE,
+        lambda K: S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                                np.zeros(B, np.uint8), maxit=K, tol=0.0))
+    print("worst error / gate (ratio, K, problem, vector, error, floor):", rows[:4])
+    assert rows[0][0] <= 1.0, rows[:6]
+
+
 def test_oracle_reproduces_chaos_floor(oracle):
     """The committed chaos floor (tests/golden/c2_chaos_floor.json, the outcome
     gates' rule) is what make_chaos_floor.py computes: one of its

@@ -259,6 +259,25 @@ def test_c4_trajectory_k1_to_k5_fixture():
     print("worst error/tolerance ratios:", sorted(worst, reverse=True)[:3])
 
 
+@pytest.mark.parametrize("xi", [False, True])
+def test_c4_trajectory_at_its_rounding_floor(oracle, xi):
+    """C4 at its bench K (4 problems, K = 1..5) against the oracle in the
+    blocked kernel's operation order -- F_STRUCTURED | F_CHOLSOLVE, or with
+    SOCP_F_EXPLICIT_INVERSE F_STRUCTURED | F_INV_YTY (Li = Y'Y, Y = L^-1) --
+    gated by the oracle's own sensitivity to one rounding (G +-1 ulp, three
+    seeds) instead of kappa_2(H): rel <= 10 floor_K + 1e-13
+    (tests/problems.py trajectory_at_floor)."""
+    from problems import trajectory_at_floor
+    cfg, B = C4, 4
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    flags = oracle.F_STRUCTURED | (oracle.F_INV_YTY if xi else oracle.F_CHOLSOLVE)
+    rows = trajectory_at_floor(oracle, cfg, d, B, cfg.fixed_k, flags,
+                               lambda K: run(cfg, d, maxit=K, tol=0.0, sing=np.zeros(B, np.uint8),
+                                             explicit_inverse=xi))
+    print("worst error / gate (ratio, K, problem, vector, error, floor):", rows[:4])
+    assert rows[0][0] <= 1.0, rows[:6]
+
+
 def test_c4_full_batch_properties():
     """The BASELINE C4 batch (1,024 problems, fixed-K=5, device-resident): every
     problem runs its 5 iterations and stays strictly inside its 8 cones."""

@@ -129,3 +129,20 @@ def test_explicit_inverse_split_equals_fused_c2(oracle):
     for key in ("cx", "cy", "cz", "cs"):
         assert np.array_equal(split[key], fused[key]), key
         assert rel(fused[key], dflt[key]) <= 1e-9, (key, rel(fused[key], dflt[key]))
+
+
+@pytest.mark.parametrize("cfg", [C1, C2], ids=["C1", "C2"])
+def test_explicit_inverse_trajectory_at_its_rounding_floor(oracle, cfg):
+    """The explicit-inverse kernel through the bench K against the oracle in its
+    own operation order (X = W^-1 G, Li = Y'Y with Y = L^-1: F_STRUCTURED |
+    F_INV_YTY), gated by the oracle's sensitivity to one rounding:
+    rel <= 10 floor_K + 1e-13 for every K, vector and problem (8 problems)."""
+    from problems import trajectory_at_floor
+    B = 8
+    d = oracle.generate(cfg.cones, B, cfg.n, cfg.m, cfg.k, cfg.seed)
+    rows = trajectory_at_floor(
+        oracle, cfg, d, B, cfg.fixed_k, oracle.F_STRUCTURED | oracle.F_INV_YTY,
+        lambda K: S.batch_solve(cfg.cones, cfg.n, cfg.m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"],
+                                np.zeros(B, np.uint8), maxit=K, tol=0.0, explicit_inverse=True))
+    print("worst error / gate (ratio, K, problem, vector, error, floor):", rows[:4])
+    assert rows[0][0] <= 1.0, rows[:6]
