@@ -1302,6 +1302,203 @@ struct Small {
     return __any(dm);
   }
 
+#ifndef SOCP_RESID_SCAL
+#define SOCP_RESID_SCAL 1  // MP_ITER: residuals and compute_scaling interleaved (0: back to back)
+#endif
+  // The per-cone SOC branch of compute_scaling (scalings.jl:32-99) on cone lane
+  // c = lane, computed on every lane (branch-free: its instructions share the
+  // caller's scheduling region) and stored by the SOC cone lanes only.
+  struct ScalCone1 {
+    double mu, im, wb0, i1, l0, as, az, bs, bz;
+    bool dm;
+  };
+  __device__ __forceinline__ ScalCone1 scal_cone1_math(int o, int c) const {
+    ScalCone1 r;
+    const double z0 = LDS(Z_ + o), s0 = LDS(S_ + o);
+    const double onrmz = z0 * z0 - cone_tot(0, c), onrms = s0 * s0 - cone_tot(1, c);
+    const double fz = rsqrt_nr(onrmz), fs = rsqrt_nr(onrms);
+    const double nrmz = onrmz * fz, nrms = onrms * fs;
+    const double zb0 = z0 * fz, sb0 = s0 * fs;
+    const double nsum = zb0 * sb0 + cone_tot(2, c) * fz * fs;
+    const double garg = (1.0 + nsum) * 0.5;
+    const double rg = rsqrt_nr(garg);
+    const double gamma = garg * rg;
+    const double fg = 0.5 * rg;
+    r.wb0 = (sb0 + zb0) * fg;
+    const double ratio = nrms * fz, prod = nrms * nrmz;
+    r.im = rsqrt_nr(ratio);
+    r.mu = ratio * r.im;
+    const double tmv1 = sqrt_nr(prod);
+    const double mult = tmv1 * recip(zb0 + sb0 + 2.0 * gamma);
+    r.l0 = gamma * tmv1;
+    r.dm = (onrmz < 0.0) || (onrms < 0.0) || (garg < 0.0) || (ratio < 0.0) || (prod < 0.0);
+    r.i1 = recip(1.0 + r.wb0);
+    r.as = fs * fg;
+    r.az = fz * fg;
+    r.bs = fs * (gamma + zb0) * mult;
+    r.bz = fz * (gamma + sb0) * mult;
+    return r;
+  }
+  __device__ __forceinline__ void scal_cone1_store(const ScalCone1& r, int o, int c) {
+    LDS(cc(CC_MU, c)) = r.mu;
+    LDS(cc(CC_IMU, c)) = r.im;
+    LDS(cc(CC_WB0, c)) = r.wb0;
+    LDS(cc(CC_I1, c)) = r.i1;
+    LDS(cc(CC_L0, c)) = r.l0;
+    LDS(cc(CC_AS, c)) = r.as;  // wbar_i = (s_i/|s| - z_i/|z|) / (2 gamma)
+    LDS(cc(CC_AZ, c)) = r.az;
+    LDS(cc(CC_BS, c)) = r.bs;  // lambda_i (scalings.jl:91-97)
+    LDS(cc(CC_BZ, c)) = r.bz;
+    LDS(WB + o) = r.wb0;
+    LDS(LAM + o) = r.l0;
+    LDS(CA + o) = -r.im;
+    LDS(CBV + o) = -(1.0 + r.wb0) * r.im;
+  }
+
+  // gemv_Gt hook: the cone-lane chain in the first batch of G'z
+  struct ScalHook {
+    Small& S;
+    ScalCone1& r;
+    int o, c;
+    template <int B>
+    __device__ __forceinline__ void run() {
+      if constexpr (B == 0) r = S.scal_cone1_math(o, c);
+    }
+  };
+
+  // MP_ITER: the residuals (solver.jl:109-118) and compute_scaling (:106) with
+  // ds = lam o lam (:120) in one pass.  They are independent (the scaling
+  // reads z and s, the residuals x, y, z, s), so their phases share
+  // scheduling regions: the scaling's cone-lane chains (rsqrt / recip
+  // latency on three lanes) run inside the residuals' G'z pass and beside
+  // their G x pass (VALU issue), the element part beside the A products (LDS
+  // latency).  The same operations as residuals() then scaling_op(): the
+  // results are bitwise the same.  Returns the DomainError flag.
+  __device__ __forceinline__ bool resid_scaling(double& nd, double& np_, double& gap, double& ll, bool& dm_aa) {
+    MARK_BEGIN("resid_scaling");
+    LANE_IDS();
+    constexpr int NS = KP > 64 ? 2 : 1;
+    double cq[NQ], xq[NQ], zv[NS], sv[NS];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      cq[q] = LDS(C_ + 16 * q + cl);
+      xq[q] = LDS(X_ + 16 * q + cl);
+    }
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      zv[t] = LDS(Z_ + 64 * t + lane);
+      sv[t] = LDS(S_ + 64 * t + lane);
+    }
+    // ---- scaling, first reduction: |z_1|^2, |s_1|^2, z_1's_1 per cone
+    double v[2][3], zi[2], si[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane;
+      zi[s] = LDS(Z_ + i);
+      si[s] = LDS(S_ + i);
+      const bool tail = kd[s] == 2;
+      v[s][0] = tail ? zi[s] * zi[s] : 0.0;
+      v[s][1] = tail ? si[s] * si[s] : 0.0;
+      v[s][2] = tail ? zi[s] * si[s] : 0.0;
+    }
+    cone_partials<3>(v);
+    // ---- the cone-lane chain inside G'z's first batch
+    const bool socl = HOIST_CST ? lc_soc : (lane < nc && (int)LDS(O_CKIND + lane) == SOC_K);
+    const int cc_ = lane < nc ? lane : 0;
+    const int oc = socl ? (HOIST_CST ? lc_off : (int)LDS(O_COFF + lane)) : 0;
+    ScalCone1 c1;
+    double acc[NQ], at[NQ];
+    gemv_Gt(Z_, acc, ScalHook{*this, c1, oc, cc_});
+    if (socl) scal_cone1_store(c1, oc, cc_);
+    bool dm = socl && c1.dm;
+    SYNC();
+    // ---- the elements (POC, scalings.jl:22-30; SOC tails) beside A'y
+    MARK_BEGIN("scal_elem");
+    double li[2], wbi[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = 64 * s + lane, c = ci[s];
+      const bool poc = kd[s] == 0, tail = kd[s] == 2;
+      const double pr = si[s] * zi[s];
+      const double q = rsqrt_nr(pr);
+      const double as = ccv(CC_AS, c), az = ccv(CC_AZ, c), bs = ccv(CC_BS, c), bz = ccv(CC_BZ, c);
+      const double imu = ccv(CC_IMU, c), l0 = ccv(CC_L0, c);
+      const double wt = si[s] * as - zi[s] * az;
+      const double lt = si[s] * bs + zi[s] * bz;
+      dm = dm || (poc && pr < 0.0);
+      wbi[s] = poc ? zmul(si[s], q) : (tail ? wt : ccv(CC_WB0, c));
+      li[s] = poc ? zmul(pr, q) : (tail ? lt : l0);
+      if (poc || tail) {
+        LDS(WB + i) = wbi[s];
+        LDS(LAM + i) = li[s];
+        LDS(CA + i) = poc ? zmul(zi[s], q) : imu;
+        LDS(CBV + i) = poc ? 0.0 : wt * imu;
+        if (poc) LDS(IL + i) = q;
+        LDS(DS + i) = -(poc ? li[s] * li[s] : (l0 * li[s] + l0 * li[s]));  // -ds: the RHS
+      }
+      v[s][0] = (poc || tail) ? li[s] * li[s] : 0.0;
+      v[s][1] = tail ? wbi[s] * wbi[s] : 0.0;
+      v[s][2] = tail ? wbi[s] * li[s] : 0.0;
+    }
+    At_mv(Y_, at);
+    cone_partials<3>(v);
+    // ---- rd, the second cone-lane part beside A x and G x + s - h
+    double d2 = 0.0, zs = 0.0;
+    if (g == 0) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int j = 16 * q + cl;
+        if (j < n) {
+          const double vv = (at[q] + acc[q]) + cq[q];
+          LDS(RD + j) = -vv;  // the residuals are stored negated: the affine RHS (solver.jl:124)
+          d2 = fma(vv, vv, d2);
+        }
+      }
+    }
+    const double p2 = A_mv(X_, B_, RP, O_A, true);
+    bool da = false;
+    double tl = 0.0;
+    {
+      MARK_BEGIN("scal_cone2");
+      const double l1 = cone_tot(0, cc_);
+      const double l0 = LDS(cc(CC_L0, cc_));
+      const double aa = l0 * l0 - l1;
+      const double sa = rsqrt_nr(aa);
+      const double w2 = cone_tot(1, cc_), wl = cone_tot(2, cc_);
+      const double iaa = recip(aa), il0 = recip(l0), il0aa = recip(l0 * aa), sal = recip(sa * l0 + 1.0);
+      gemv_G_r<true>(xq, S_, H_, DZ);
+      if (lane < nc) {
+        if (socl) {
+          da = aa < 0.0;
+          LDS(cc(CC_W2, cc_)) = w2;
+          LDS(cc(CC_WL, cc_)) = wl;
+          LDS(cc(CC_AA, cc_)) = aa;
+          LDS(cc(CC_IAA, cc_)) = iaa;
+          LDS(cc(CC_IL0, cc_)) = il0;
+          LDS(cc(CC_IL0AA, cc_)) = il0aa;
+          LDS(cc(CC_SA, cc_)) = sa;
+          LDS(cc(CC_SAL, cc_)) = sal;
+          tl = l0 * l0 + l1;
+          LDS(DS + oc) = -tl;
+        } else {
+          tl = l1;
+        }
+      }
+    }
+    SYNC();
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+      if (64 * t + lane < k) zs += zv[t] * sv[t];
+    double r3[3] = {d2, p2, zs};  // the three whole-wave sums in one interleaved scan
+    dpp_scan<3>(r3, lane, 0, false);
+    nd = sqrt(readlane_d(r3[0], 63));
+    np_ = sqrt(readlane_d(r3[1], 63));
+    gap = readlane_d(r3[2], 63);
+    ll = wsum(tl);
+    dm_aa = __any(da);
+    return __any(dm);
+  }
+
   // First half of solve_kkt(::DenseSolver) (densesolver.jl:61-66):
   //   k0 = lam^-1 o ds (iprod!), k1 = W k0 (scale!), k2 = dz - k1,
   //   t2 = iWiW k2 = W^-1 (W^-1 k2).
@@ -2690,8 +2887,15 @@ struct Small {
 
   // acc[q] (all lanes) = (G' v)[16q+cl].  The v reads of the next batch of
   // row steps are issued before the current batch's products (one exposed
-  // LDS round trip per call, not one per pair of row steps).
-  __device__ __forceinline__ void gemv_Gt(int v, double (&acc)[NQ]) {
+  // LDS round trip per call, not one per pair of row steps).  hook.run<b>()
+  // runs inside batch b's scheduling region (b < 2): independent work whose
+  // latency the batch's VALU stream hides (resid_scaling).
+  struct NoGtHook {
+    template <int B>
+    __device__ __forceinline__ void run() {}
+  };
+  template <class HK = NoGtHook>
+  __device__ __forceinline__ void gemv_Gt(int v, double (&acc)[NQ], HK&& hook = HK()) {
     MARK_BEGIN("gemv_Gt");
     LANE_IDS();
     constexpr int VB = 8;
@@ -2706,6 +2910,8 @@ struct Small {
 #pragma unroll
       for (int j = 0; j < VB; ++j) vn[j] = p0 + VB + j < NP ? LDS(v + 4 * (p0 + VB + j) + g) : 0.0;
       SCHED_FENCE();
+      if (p0 == 0) hook.template run<0>();
+      if (p0 == VB) hook.template run<1>();
 #pragma unroll
       for (int j = 0; j < VB; ++j) {
         if (p0 + j < NP) {
@@ -3232,17 +3438,28 @@ struct Small {
             done = true;
             break;
           }
-          if (SOCP_KO & 2) {
-            nd = np_ = gap = 1.0;
+          bool dm;
+          if constexpr (SOCP_RESID_SCAL && !(SOCP_KO & (2 | 4096))) {
+            // (after the last iteration the scaling is computed too, and unused)
+            dm = resid_scaling(nd, np_, gap, ll, dm_aa);
+            STAMP(SP_RESID);
+            if (it >= a.maxit) {
+              done = true;
+              break;
+            }
           } else {
-            residuals(nd, np_, gap);
+            if (SOCP_KO & 2) {
+              nd = np_ = gap = 1.0;
+            } else {
+              residuals(nd, np_, gap);
+            }
+            STAMP(SP_RESID);
+            if (it >= a.maxit) {
+              done = true;
+              break;
+            }
+            dm = scaling_op(ll, dm_aa, true);
           }
-          STAMP(SP_RESID);
-          if (it >= a.maxit) {
-            done = true;
-            break;
-          }
-          const bool dm = scaling_op(ll, dm_aa, true);
           STAMP(SP_VOP);
           if (dm) {
             status = ST_DOMAIN;
