@@ -48,8 +48,9 @@ def flops_executed_per_problem_iter(n, m, k, sing=False, large=False):
     m <= 16, densesolver.jl:47 cholesky! + triangular solves; the blocked
     kernel's default SOCP_LG_CHOL build) potrf is n^3/3 and Z = L^-1 A' is
     m n^2, in place of potrf + potri (n^3) and A*Li (2 m n^2) of the SURVEY.md
-    §8(d) formula; the Gauss-Jordan sweep path (register kernel, m > 16) forms
-    Li and executes the formula's figure."""
+    §8(d) formula; where Li is formed (the register kernel for m > 16, and
+    --explicit-inverse: potrf + trtri + lauum from the one factor, chol_inv)
+    the kernel executes the formula's figure."""
     if not (large or m <= 16):
         return flops_per_problem_iter(n, m, k, sing)
     return (n * (n + 1) * k + n ** 3 / 3.0 + m * n * n + m * (m + 1) * n + m ** 3 / 3.0
