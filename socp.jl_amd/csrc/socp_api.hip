@@ -1078,6 +1078,9 @@ extern "C" int socp_sqr_solve_kkt(socp_sqr* h, const double* dx, const double* d
 // the launches once it stops (socp_sqr_ipm.hip).  c, b, h in; x, y, z, s,
 // iters, status (and res: ||rd||, ||rp||, z's at the returned iterate, may be
 // NULL) out; host or device pointers as the handle's flags say.
+#ifndef SQR_FUSE_RESID
+#define SQR_FUSE_RESID 1  // 0: the separate residual kernel after every setup launch (A/B builds)
+#endif
 extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b, const double* hv,
                                    const socp_params* params, double* x, double* y, double* z, double* s,
                                    int32_t* iters, int32_t* status, double* res) {
@@ -1169,9 +1172,19 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
   TRY(ipm(1, 0));
   su.active = ia.active;
   sv.active = ia.active;
+  // the wavefront setup kernel computes the residuals in its pass over G and
+  // takes the resid kernel's exit test and right-hand side (SqrArgs::fuse_resid)
+  const bool fuse = !h->L.large && SQR_FUSE_RESID;
+  if (fuse) {
+    su.fuse_resid = 1;
+    su.ix = ia.x; su.iy = ia.y; su.ic = ia.c; su.ib = ia.b; su.ih = ia.h;
+    su.odx = ia.dx; su.ody = ia.dy; su.odz = ia.dz; su.ods = ia.ds; su.ores = ia.res;
+    su.ostatus = ia.status; su.oactive = ia.active; su.n_active = ia.n_active;
+    su.tol = P.tol;
+  }
   for (int it = 0; it < P.maxit; ++it) {
-    TRY(sqr_launch(h, su, true, false));   // compute_scaling + setup_iter
-    TRY(ipm(2, it));                       // residuals, exit test, affine right-hand side
+    TRY(sqr_launch(h, su, true, false));   // compute_scaling + setup_iter (+ fused: the residuals)
+    if (!fuse) TRY(ipm(2, it));            // residuals, exit test, affine right-hand side
     TRY(sqr_launch(h, sv, false, false));  // solve_kkt (affine)
     TRY(ipm(3, it));                       // step, sigma, mu, corrector right-hand side
     TRY(sqr_launch(h, sv, false, false));  // solve_kkt (combined)

@@ -339,10 +339,13 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
 #ifdef SOCP_DIAG
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
+  double zs = 0.0;  // s'z for the fused residuals (s, z's LDS is reused by the G'u / G'v below)
   for (int i = lane; i < k; i += 64) {
-    lds[L.o_s + i] = a.s[p * k + i];
-    lds[L.o_z + i] = a.z[p * k + i];
+    const double si = a.s[p * k + i], zi = a.z[p * k + i];
+    lds[L.o_s + i] = si;
+    lds[L.o_z + i] = zi;
     lds[L.o_one + i] = 1.0;
+    zs = fma(zi, si, zs);
   }
   if (lane == 0) lds[L.o_flag] = 0.0;
   wsync();
@@ -380,6 +383,19 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
       }
       wsync();
     }
+  }
+  // fused residuals (a.fuse_resid): this lane's elements of a staged G chunk
+  // are row r0 + (lane & 7) of the columns (lane >> 3) + 8 q; gz[q]
+  // accumulates those columns' G'z, and each chunk's row sums of G x are
+  // reduced over the eight lanes that share the row
+  constexpr int PEF = SQR_KC * NC / 64;
+  const bool FR = a.fuse_resid != 0;
+  double xq[PEF], gz[PEF];
+#pragma unroll
+  for (int q = 0; q < PEF; ++q) {
+    const int col = (lane >> 3) + 8 * q;
+    xq[q] = (FR && col < n) ? a.ix[p * n + col] : 0.0;
+    gz[q] = 0.0;
   }
   if (status == 0) {
     // ---- H = G'DG (+A'A) on f64 MFMA 16x16x4: the lower 16x16 tiles,
@@ -423,6 +439,23 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
           const bool in = r0 + r < rows;
           Ya[r * SQR_NW + col] = pass ? g : (in ? fa[r0 + r] * g : 0.0);
           Yb[r * SQR_NW + col] = pass ? g : (in ? fb[r0 + r] * g : 0.0);
+        }
+        if (FR && pass == 0) {
+          const int row = r0 + (lane & 7);
+          const double zr = row < k ? lds[L.o_z + row] : 0.0;
+          double gxr = 0.0;
+          static_assert(PE == PEF, "chunk elements per lane");
+#pragma unroll
+          for (int q = 0; q < PE; ++q) {
+            gz[q] = fma(gn[q], zr, gz[q]);
+            gxr = fma(gn[q], xq[q], gxr);
+          }
+          gxr += row_partner<8>(gxr);
+          gxr = rows_sum(gxr);  // (G x)[row] in the eight lanes of the row
+          if (lane < 8 && row < k) {
+            const double v = gxr + lds[L.o_s + row] - a.ih[p * k + row];  // rz (solver.jl:118)
+            a.odz[p * k + row] = -v;  // stored negated: the affine right-hand side (solver.jl:124)
+          }
         }
 #pragma unroll
         for (int q = 0; q < PE; ++q) {  // the next chunk's loads fly under this chunk's MFMAs
@@ -641,6 +674,38 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
       SQ_STAMP(5);
     }
   }
+  // ---- fused residuals: rd = A'y + G'z + c, rp = A x - b, the norms
+  double r3[3] = {0.0, 0.0, 0.0};
+  if (a.fuse_resid && status != SQR_DOMAIN) {
+    // G'z: each column's eight row-lane partials (lanes 8j .. 8j+7)
+    double d2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < PEF; ++q) {
+      double v = gz[q];
+      v += row_partner<4>(v);
+      v += row_partner<2>(v);
+      v += row_partner<1>(v);
+      const int col = (lane >> 3) + 8 * q;
+      if ((lane & 7) == 0 && col < n) {
+        double aty = 0.0;
+        for (int r = 0; r < m; ++r) aty = fma(A[(int64_t)col * m + r], a.iy[p * m + r], aty);
+        const double rd = (aty + v) + a.ic[p * n + col];
+        a.odx[p * n + col] = -rd;
+        d2 = fma(rd, rd, d2);
+      }
+    }
+    double p2 = 0.0;
+    if (lane < m) {
+      double ax = 0.0;
+      for (int j = 0; j < n; ++j) ax = fma(A[(int64_t)j * m + lane], a.ix[p * n + j], ax);
+      const double rp = ax - a.ib[p * m + lane];
+      a.ody[p * m + lane] = -rp;
+      p2 = rp * rp;
+    }
+    r3[0] = sqrt(wave_sum(d2));
+    r3[1] = sqrt(wave_sum(p2));
+    r3[2] = wave_sum(zs);
+  }
   // ---- the factor record
   if (status == 0) {
     // the lower triangle only: the record's upper triangle is zeroed once by
@@ -666,6 +731,46 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
   if (lane == 0) {
     rec[L.r_st] = (double)status;
     a.status[p] = status;
+  }
+  if (a.fuse_resid) {
+    // socp_sqr_ipm_resid_kernel's decisions (solver.jl:106-125): the scaling's
+    // DomainError first, then the exit test, then the factorisation's status
+    int fin = -1;
+    if (status == SQR_DOMAIN) {
+      fin = SQR_DOMAIN;
+    } else {
+      if (lane == 0) {
+        a.ores[3 * p + 0] = r3[0];
+        a.ores[3 * p + 1] = r3[1];
+        a.ores[3 * p + 2] = r3[2];
+      }
+      if (r3[0] + r3[1] + r3[2] < a.tol)
+        fin = 0;
+      else if (status != 0)
+        fin = status;
+    }
+    if (fin >= 0) {
+      if (lane == 0) {
+        a.ostatus[p] = fin;
+        a.oactive[p] = 0;
+        atomicSub(a.n_active, 1);  // the host stops launching once none is left
+      }
+    } else {
+      // ds = -(lam o lam) (vprod!, vectors.jl:58-81; the affine right-hand side)
+      const double* lam = lds + L.o_l;
+      for (int c = 0; c < nc; ++c) {
+        const int o = a.cones.offs[c], d = a.cones.dim[c];
+        if (a.cones.kind[c] == POC_K) {
+          for (int i = o + lane; i < o + d; i += 64) a.ods[p * k + i] = -(lam[i] * lam[i]);
+          continue;
+        }
+        double part = 0.0;
+        for (int i = o + lane; i < o + d; i += 64) part += lam[i] * lam[i];
+        const double t0 = wave_sum(part), l0 = lam[o];
+        for (int i = o + 1 + lane; i < o + d; i += 64) a.ods[p * k + i] = -(l0 * lam[i] + l0 * lam[i]);
+        if (lane == 0) a.ods[p * k + o] = -t0;
+      }
+    }
   }
   SQ_STAMP(6);
 }

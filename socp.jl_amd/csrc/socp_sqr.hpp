@@ -121,6 +121,15 @@ struct SqrArgs {
   const int32_t* active;   // B or NULL: problems with active[p] == 0 are skipped (the batched IPM's mask)
   int32_t init;            // solve: the initial-point system (solver.jl:68-84, an exact solve in the
                            // reference): m0 = -cy also when sing, as the dense kernel's MP_INIT
+  // socp_sqr_solve_socp's iteration setup on the wavefront kernel (fuse_resid
+  // != 0): the residuals (solver.jl:109-118) ride along the setup's pass over
+  // G, and the resid kernel's exit test and affine right-hand side follow the
+  // factorisation in the same launch (socp_sqr_ipm_resid_kernel's work)
+  int32_t fuse_resid;
+  const double *ix, *iy, *ic, *ib, *ih;  // the iterate's x, y and the data c, b, h
+  double *odx, *ody, *odz, *ods, *ores;  // -rd, -rp, -rz, -lam o lam; ||rd||, ||rp||, z's
+  int32_t *ostatus, *oactive, *n_active;
+  double tol;
 };
 
 // the batched solve_socp on the rank-update plugin (socp_sqr_ipm.hip): the
