@@ -43,6 +43,18 @@
 #ifndef SOCP_LG_CATCH_SPLIT
 #define SOCP_LG_CATCH_SPLIT 1  // chol_nb: split the last panels' catch-up blocks by 16-column groups
 #endif
+#ifndef SOCP_LG_SYRK_SYNC
+#define SOCP_LG_SYRK_SYNC 128  // form_H: rows of k between workgroup barriers (0: none)
+#endif
+#ifndef SOCP_LG_SYRK_ORDER
+#define SOCP_LG_SYRK_ORDER 1  // form_H with SYRK_SYNC at NPAD = 512: the panel-sharing round order (0: row-major)
+#endif
+#ifndef SOCP_LG_ZU_SYNC
+#define SOCP_LG_ZU_SYNC 0  // chol_fwd_multi: rows of L between workgroup barriers (0: none)
+#endif
+#ifndef SOCP_LG_CATCH_SYNC
+#define SOCP_LG_CATCH_SYNC 0  // chol_nb's catch-up: panels between workgroup barriers (0: none)
+#endif
 #ifndef SOCP_LG_SYRK_UNROLL
 #define SOCP_LG_SYRK_UNROLL 1  // blk_gemm's k loop (16 rows per step)
 #endif
@@ -1182,8 +1194,66 @@ struct Large {
 
   // H = X'X (+A'A) (densesolver.jl:42-46): lower 64x64 blocks, one wavefront
   // per block; padding diagonal = 1.
+  __device__ __forceinline__ static int syrk_order8(int t) {
+    // (I << 3) | J of the t-th block, rounds of eight (form_H)
+    constexpr unsigned char tab[36] = {
+        0x00, 0x08, 0x09, 0x10, 0x11, 0x12, 0x18, 0x19,  // panels 0..3
+        0x24, 0x2c, 0x2d, 0x34, 0x35, 0x36, 0x3c, 0x3d,  // panels 4..7
+        0x20, 0x21, 0x22, 0x23, 0x28, 0x29, 0x2a, 0x2b,  // {4,5} x {0..3}
+        0x30, 0x31, 0x32, 0x33, 0x38, 0x39, 0x3a, 0x3b,  // {6,7} x {0..3}
+        0x1a, 0x1b, 0x3e, 0x3f};                         // (3,2) (3,3) (7,6) (7,7)
+    return tab[t];
+  }
   __device__ void form_H(bool addAA) {
     const int NB = L.NPAD / 64, nblk = NB * (NB + 1) / 2;
+#if SOCP_LG_SYRK_SYNC > 0
+    // The eight wavefronts' blocks of one round share X panels (row-major
+    // lower triangle: round 1 reads panels 0..3 for 8 blocks), but a panel
+    // row is in L2 only while the wavefronts are within a few k-steps of one
+    // another.  A workgroup barrier every SOCP_LG_SYRK_SYNC rows of k keeps
+    // them in step, so a round reads each of its panels from HBM once instead
+    // of once per block.  Idle wavefronts of the last round keep the count.
+    if (!addAA) {
+      constexpr int KB = SOCP_LG_SYRK_SYNC;
+      const int KP = L.KP;
+      for (int r = 0; r < nblk; r += NW) {
+        const int t = r + wv;
+        int I = 0, J = 0;
+        if (t < nblk) {
+          if (SOCP_LG_SYRK_ORDER && NB == 8 && NW == 8) {
+            // rounds over few panels: the 0..3 and 4..7 triangles (4 panels
+            // each), {4,5} x {0..3} and {6,7} x {0..3} (6 each), the rest (4):
+            // 24 panel reads per SYRK instead of the row-major order's 30
+            const int code = syrk_order8(t);
+            I = code >> 3;
+            J = code & 7;
+          } else {
+            tri_ij(t, I, J);
+          }
+        }
+        d4 acc[4][4];
+        zero_blk(acc);
+        for (int k0 = 0; k0 < KP; k0 += KB) {
+          const int kr = KP - k0 < KB ? KP - k0 : KB;
+          if (t < nblk) {
+            if (I == J)
+              blk_gemm<true>(acc, Xw + k0, Xw + k0, KP, 64 * I, 64 * J, kr, true, -1);
+            else
+              blk_gemm(acc, Xw + k0, Xw + k0, KP, 64 * I, 64 * J, kr, false, -1);
+          }
+          __builtin_amdgcn_s_barrier();
+        }
+        if (t < nblk) {
+          if (I == J)
+            store_blk<true>(acc, Hm, L.NPAD, 64 * I, 64 * J, n);
+          else
+            store_blk(acc, Hm, L.NPAD, 64 * I, 64 * J, n);
+        }
+      }
+      BAR();
+      return;
+    }
+#endif
     for (int t = wv; t < nblk; t += NW) {
       int I, J;
       tri_ij(t, I, J);
@@ -1404,6 +1474,36 @@ struct Large {
       if (P > 0 && SOCP_LG_CATCH_SPLIT && SOCP_LG_CATCH_SPLIT_K * (nb - P) <= NW) {
         // few blocks left: each block's catch-up split into its four 16-column
         // groups, one per wavefront (bitwise the whole-block result)
+#if SOCP_LG_CATCH_SYNC > 0
+        if (4 * (nb - P) <= NW) {
+          // one item per wavefront: the items share panel Q's rows, read in
+          // step (see the whole-block case below)
+          const int it = wv, t = P + it / 4, a_ = it % 4;
+          const bool act = it < 4 * (nb - P);
+          d4 acc[4];
+          if (act) {
+            if (t == P)
+              load_colT<true>(acc, M, ld, 64 * t, 64 * P, a_);
+            else
+              load_colT(acc, M, ld, 64 * t, 64 * P, a_);
+          }
+          for (int Q = 0; Q < P; ++Q) {
+            if (act) {
+              if (t == P)
+                gram_colT<true>(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q, a_);
+              else
+                gram_colT(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q, a_);
+            }
+            if ((Q + 1) % SOCP_LG_CATCH_SYNC == 0) __builtin_amdgcn_s_barrier();
+          }
+          if (act) {
+            if (t == P)
+              store_colT<true>(acc, M, ld, 64 * t, 64 * P, a_);
+            else
+              store_colT(acc, M, ld, 64 * t, 64 * P, a_);
+          }
+        } else
+#endif
         for (int it = wv; it < 4 * (nb - P); it += NW) {
           const int t = P + it / 4, a_ = it % 4;
           d4 acc[4];
@@ -1419,6 +1519,38 @@ struct Large {
         }
         BAR();
       } else if (P > 0) {
+#if SOCP_LG_CATCH_SYNC > 0
+        if (nb - P <= NW) {
+          // one block per wavefront, and every block reads panel Q's rows of
+          // the P block: with the wavefronts in step (a barrier every
+          // SOCP_LG_CATCH_SYNC panels) those rows come from L2 after the
+          // first reader
+          const int t = P + wv;
+          const bool act = t < nb;
+          d4 acc[4][4];
+          if (act) {
+            if (t == P)
+              load_blkT<true>(acc, M, ld, 64 * t, 64 * P);
+            else
+              load_blkT(acc, M, ld, 64 * t, 64 * P);
+          }
+          for (int Q = 0; Q < P; ++Q) {
+            if (act) {
+              if (t == P)
+                gram_blkT<true>(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q);
+              else
+                gram_blkT(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q);
+            }
+            if ((Q + 1) % SOCP_LG_CATCH_SYNC == 0) __builtin_amdgcn_s_barrier();
+          }
+          if (act) {
+            if (t == P)
+              store_blkT<true>(acc, M, ld, 64 * t, 64 * P);
+            else
+              store_blkT(acc, M, ld, 64 * t, 64 * P);
+          }
+        } else
+#endif
         for (int t = P + wv; t < nb; t += NW) {
           d4 acc[4][4];
           if (t == P) {
@@ -1610,6 +1742,10 @@ struct Large {
     const int NB = L.NPAD / 64, MT = L.MPAD / 16, MP = L.MPAD;
     gdbl* const Rs = Yp;
     const d4 zero = {0.0, 0.0, 0.0, 0.0};
+    // SOCP_LG_ZU_SYNC: when every wavefront has the same number of tiles, a
+    // workgroup barrier every SOCP_LG_ZU_SYNC rows keeps the tiles that share
+    // rows of L (same ta) or of Z (same tb) in step, so they meet in L2
+    const bool zsync = SOCP_LG_ZU_SYNC > 0 && (4 * MT) % NW == 0;
     for (int P = 0; P < NB; ++P) {
       const int P0 = 64 * P;
       for (int tt = wv; tt < 4 * MT; tt += NW) {
@@ -1622,6 +1758,8 @@ struct Large {
         // memory round trip per 32 rows instead of per 8); acc0 / acc1 take the
         // same rows in the same order as before
         for (int y0 = 0; y0 < P0; y0 += 4 * SOCP_LG_ZU) {
+          if (SOCP_LG_ZU_SYNC > 0 && zsync && y0 > 0 && y0 % (SOCP_LG_ZU_SYNC > 0 ? SOCP_LG_ZU_SYNC : 1) == 0)
+            __builtin_amdgcn_s_barrier();
           double a[SOCP_LG_ZU], b[SOCP_LG_ZU];
 #pragma unroll
           for (int u = 0; u < SOCP_LG_ZU; ++u) {
