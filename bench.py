@@ -452,6 +452,10 @@ def main(argv=None):
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default: the newest profiles/rNN_pmc_traffic[_<config>].json")
     ap.add_argument("--stub-solve", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group of an N > 1 run: nccl (= RCCL, one GPU per rank; the product line) or "
+                         "gloo (rehearsal: the ranks may share GPUs, outcomes exchanged through host memory; "
+                         "the line says so and is not a scaling measurement)")
     args = ap.parse_args(argv)
     argv = sys.argv[1:] if argv is None else list(argv)
     if args.gpus < 1:
@@ -484,8 +488,11 @@ def run_rank(args, world):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     stub = args.stub_solve
+    rehearsal = world > 1 and not stub and args.dist_backend == "gloo"
+    if rehearsal:
+        local = local % max(1, torch.cuda.device_count())  # ranks may share a GPU
     if world > 1:
-        if stub:
+        if stub or rehearsal:
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
@@ -578,11 +585,14 @@ def run_rank(args, world):
                                f"value counts executed iterations)" if ref_rule else
                                f"initial point + fixed-K={K} IPM iterations (tol=0)")
                             + ("; explicit inverse Li = H^-1 (SOCP_F_EXPLICIT_INVERSE, the reference's "
-                               "op order, densesolver.jl:47-48: potrf, then potrs against I)"
+                               "op order, densesolver.jl:47-48: Li from the Cholesky factor, L^-T L^-1)"
                                if args.explicit_inverse else ""),
                 "operation_order": "explicit_inverse" if args.explicit_inverse else "cholesky",
                 "global_batch": B * world,
-                "parallelism": f"dp{world} (disjoint problem shards, status all-gather only)",
+                "parallelism": f"dp{world} (disjoint problem shards, status all-gather only)"
+                               + ("; REHEARSAL: gloo process group, ranks sharing "
+                                  f"{torch.cuda.device_count()} GPU(s) -- not a scaling measurement"
+                                  if rehearsal else ""),
             },
             "kernel": kname,
             "kernel_ms": kms,
@@ -606,6 +616,12 @@ def run_rank(args, world):
                 "problem_iters_per_launch": iters_per_launch,
             },
         }
+        if world > 1 and tr.get("gathered") is not None:
+            # every rank's outcome records as rank 0 received them (the exchange step)
+            gst = tr["gathered"]["status"].reshape(-1).long().cpu()
+            line["gathered"] = {"status_counts": torch.bincount(gst, minlength=5).tolist(),
+                                "iters_sum": int(tr["gathered"]["iters"].long().sum().item()),
+                                "problems": int(gst.numel())}
         extras = world == 1 and not stub
         if extras and not args.no_ingest:
             line["ingest"] = ingest_line(S, cfg, B, K, tol, (c, A, b, G, h), args.steps, ctx)

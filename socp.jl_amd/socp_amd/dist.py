@@ -53,9 +53,12 @@ def gather_outcomes(status, iters, res=None, group=None):
     import torch.distributed as dist
     world = dist.get_world_size(group)
     local = pack_outcomes(status, iters, res).reshape(-1)
+    dev = local.device
+    if dist.get_backend(group) == "gloo" and dev.type != "cpu":
+        local = local.cpu()  # gloo exchanges host buffers (bench.py --dist-backend gloo rehearsal)
     out = torch.empty((world, local.numel()), dtype=torch.uint8, device=local.device)
     dist.all_gather_into_tensor(out.view(-1), local, group=group)
-    return unpack_outcomes(out.view(world, -1, RECORD_BYTES))
+    return unpack_outcomes(out.to(dev).view(world, -1, RECORD_BYTES))
 
 
 COMM_ID_BYTES = 128  # SOCP_COMM_ID_BYTES (include/socp.h)
@@ -178,6 +181,8 @@ def timed_shard_steps(solve_shard, steps: int, warmup: int, sync=None):
     iters_total = iters_local
     if world > 1:
         dev = st["out"]["iters"].device
+        if dist.get_backend() == "gloo":
+            dev = torch.device("cpu")
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())

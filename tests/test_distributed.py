@@ -278,6 +278,40 @@ def test_bench_launcher_starts_n_ranks():
     assert abs(line["value"] * dt - 2 * B * K * steps) <= 1e-6 * 2 * B * K * steps
     assert line["ms_per_step"] >= 10.0  # the stub's 10 ms per step
     assert line["cpu_baseline"] is None  # the CPU leg runs at N=1 only
+    # rank 0 holds every rank's outcome records after the exchange step
+    assert line["gathered"] == {"status_counts": [2 * B, 0, 0, 0, 0], "iters_sum": 2 * B * K, "problems": 2 * B}
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_real_solves_on_one_gpu():
+    """The N > 1 path end to end with the HIP solver on the one-GPU box:
+    `bench.py --gpus 2 --dist-backend gloo` starts two ranks (sharing the GPU;
+    the line is marked a rehearsal), each generates and solves its own shard
+    (problems rank * B ... of the generator's sequence) under the reference
+    stopping rule, and rank 0 gathers every 32-byte outcome record.  The
+    gathered outcomes must be those of one rank solving all 2 B problems:
+    the same status histogram and the same total iteration count (each
+    problem is solved independently, so sharding changes nothing)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    B = 2048
+    common = ["--mode", "reference", "--steps", "1", "--warmup", "0", "--no-cpu", "--no-ingest"]
+    two = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                          "--batch", str(B)] + common, capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert two.returncode == 0, two.stderr[-3000:]
+    one = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--batch", str(2 * B)] + common,
+                         capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert one.returncode == 0, one.stderr[-3000:]
+    l2, l1 = _bench_json(two.stdout), _bench_json(one.stdout)
+    assert l2["n_gpus"] == 2 and l2["config"]["global_batch"] == 2 * B
+    assert "REHEARSAL" in l2["config"]["parallelism"]
+    assert l2["gathered"]["problems"] == 2 * B
+    assert l2["gathered"]["status_counts"] == l1["status_counts"], (l2["gathered"], l1["status_counts"])
+    assert l2["gathered"]["iters_sum"] == l1["roofline"]["problem_iters_per_launch"]
+    assert sum(l2["status_counts"]) == B  # rank 0's own shard
 
 
 def test_bench_one_gpu_line_unchanged_shape():
