@@ -46,6 +46,15 @@
 #ifndef SOCP_LG_SYRK_SYNC
 #define SOCP_LG_SYRK_SYNC 128  // form_H: rows of k between workgroup barriers (0: none)
 #endif
+#ifndef SOCP_LG_GT_RS
+#define SOCP_LG_GT_RS 0  // gemv_Gt: four passes' 32 column sums by one reduce-scatter (0: per-column all-reduces)
+#endif
+#ifndef SOCP_LG_FX_RS
+#define SOCP_LG_FX_RS 1  // W^-1 G: the 32 cone sums of a pass by one reduce-scatter (0: 32 all-reduces)
+#endif
+#ifndef SOCP_LG_KO
+#define SOCP_LG_KO 0  // timing knock-outs of the W^-1 G phase (tuning builds only; results wrong)
+#endif
 #ifndef SOCP_LG_SYRK_ORDER
 #define SOCP_LG_SYRK_ORDER 1  // form_H with SYRK_SYNC at NPAD = 512: the panel-sharing round order (0: row-major)
 #endif
@@ -886,6 +895,43 @@ struct Large {
   __device__ bool form_X_fast_ok() const { return nc - csoc <= FX_NC && (k + 63) / 64 <= FX_R; }
   // chunked: X in 4-row chunks, chunk-major -- X[i][j] at ((i/4) NPAD + j) 4 + i%4
   // -- so a chunk is one contiguous 32 NPAD-byte run (the staged SYRK's DMA)
+  // 32 values per lane -> value q summed over the wavefront, in lanes 2q, 2q+1
+  // (v[0] on return)
+  __device__ __forceinline__ void fx_reduce_scatter(double (&v)[32]) const {
+    auto swap_add = [](double& x, double& y, bool rows) {
+      // x' = [x.lo, y.lo], y' = [x.hi, y.hi] (halves of the wave or of each 32-lane half)
+      const unsigned xl = (unsigned)__double2loint(x), xh = (unsigned)__double2hiint(x);
+      const unsigned yl = (unsigned)__double2loint(y), yh = (unsigned)__double2hiint(y);
+      const auto l = rows ? __builtin_amdgcn_permlane16_swap(xl, yl, false, false)
+                          : __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+      const auto h = rows ? __builtin_amdgcn_permlane16_swap(xh, yh, false, false)
+                          : __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+      x = __hiloint2double((int)h[0], (int)l[0]) + __hiloint2double((int)h[1], (int)l[1]);
+    };
+#pragma unroll
+    for (int j = 0; j < 16; ++j) swap_add(v[j], v[j + 16], false);  // lanes >= 32 now carry j + 16
+#pragma unroll
+    for (int j = 0; j < 8; ++j) swap_add(v[j], v[j + 8], true);  // odd rows carry j + 8
+    const int ln = lane;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool up = ln & 8;
+      const double send = up ? v[j] : v[j + 4], keep = up ? v[j + 4] : v[j];
+      v[j] = keep + row_partner<8>(send);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool up = ln & 4;
+      const double send = up ? v[j] : v[j + 2], keep = up ? v[j + 2] : v[j];
+      v[j] = keep + row_partner<4>(send);
+    }
+    {
+      const bool up = ln & 2;
+      const double send = up ? v[0] : v[1], keep = up ? v[1] : v[0];
+      v[0] = keep + row_partner<2>(send);
+    }
+    v[0] += row_partner<1>(v[0]);
+  }
   __device__ bool form_X_fast(bool chunked) {
     const int nsoc = nc - csoc;
     const int R = (k + 63) / 64;
@@ -919,6 +965,11 @@ struct Large {
       gcdbl* g0p = Gp + (int64_t)(j0 < nn ? j0 : 0) * kk;
       gdbl* x0 = Xw + (int64_t)j0 * KP;
       load_cols(gv, j0);
+#if SOCP_LG_FX_RS
+      double rsv[FX_CG * FX_NC];  // slot u * FX_NC + ci: this lane's partial of del
+#pragma unroll
+      for (int q = 0; q < FX_CG * FX_NC; ++q) rsv[q] = 0.0;
+#endif
       // per SOC cone: del = sum over the tail of wbar_i G_ij
 #pragma unroll
       for (int ci = 0; ci < FX_NC; ++ci) {
@@ -934,6 +985,10 @@ struct Large {
 #pragma unroll
           for (int u = 0; u < FX_CG; ++u) pd[u] = fma(w, gv[u][r], pd[u]);
         }
+#if SOCP_LG_FX_RS
+#pragma unroll
+        for (int u = 0; u < FX_CG; ++u) rsv[u * FX_NC + ci] = pd[u];
+#endif
         // the head value G[o][j0 + u] is already in a register (row o of the
         // loaded columns: lane o % 64, slot o / 64): a readlane instead of a
         // global load per column and cone on the wave's critical path
@@ -948,13 +1003,30 @@ struct Large {
           } else {
             gh = g0p[(int64_t)(u < nl ? u : 0) * kk + o];
           }
+#if SOCP_LG_FX_RS
+          if (ln == 0) LV(fx + 32 + u * FX_NC + ci) = gh;
+#else
+#if SOCP_LG_KO & 1  // timing knock-out (tuning builds only; results wrong): no reductions
+          const double del = pd[u];
+#else
           const double del = wave_sum(pd[u]);
+#endif
           if (ln == 0) {
             LV(fx + u * FX_NC + ci) = del;
             LV(fx + 32 + u * FX_NC + ci) = gh;
           }
+#endif
         }
       }
+#if SOCP_LG_FX_RS
+      // the 32 sums at once by a reduce-scatter over the wavefront: each level
+      // halves the values a lane carries and doubles the lanes each covers
+      // (lanes +-32 and +-16 by permlane swaps, +-8, +-4, +-2 by DPP, +-1 an
+      // all-reduce step), so that sum q ends in lanes 2q and 2q + 1 -- 124
+      // instructions instead of 32 wave-wide all-reduces
+      fx_reduce_scatter(rsv);
+      if ((ln & 1) == 0) LV(fx + (ln >> 1)) = rsv[0];
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -977,7 +1049,7 @@ struct Large {
           if (typ == 1) x = im * (wb0 * g - del);
           if (typ == 2) x = im * (g + (-gh + del * i1) * wbr[r]);
           if (u >= nl) x = 0.0;
-          if (row < KP) {
+          if (row < KP && !((SOCP_LG_KO & 2) && x != 1.2345)) {  // KO 2: no X stores (tuning builds only)
             if (chunked)
               Xw[((int64_t)(row >> 2) * NPD + j0 + u) * 4 + (row & 3)] = x;
             else
@@ -2226,6 +2298,46 @@ struct Large {
       double vr[GT_R];
 #pragma unroll
       for (int r = 0; r < GT_R; ++r) vr[r] = (lane + 64 * r < k) ? LV(vin + lane + 64 * r) : 0.0;
+#if SOCP_LG_GT_RS
+      if constexpr (CG == 8) {
+        // four passes' column sums (32) reduced at once by fx_reduce_scatter
+        for (int jb = CG * wv; jb < n; jb += 4 * CG * NW) {
+          double rsv[32];
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const int j0 = jb + p * CG * NW;
+            if (j0 >= n) {  // wave-uniform
+#pragma unroll
+              for (int u = 0; u < CG; ++u) rsv[p * CG + u] = 0.0;
+              continue;
+            }
+            gcdbl* g0 = Gp + (int64_t)j0 * k;
+            const int nl = n - j0;
+            double gv[CG][GT_R];
+#pragma unroll
+            for (int u = 0; u < CG; ++u)
+#pragma unroll
+              for (int r = 0; r < GT_R; ++r) {
+                const int row = lane + 64 * r;
+                gv[u][r] = (row < k) ? g0[(int64_t)(u < nl ? u : 0) * k + row] : 0.0;
+              }
+#pragma unroll
+            for (int u = 0; u < CG; ++u) {
+              double acc = 0.0;
+#pragma unroll
+              for (int r = 0; r < GT_R; ++r) acc = fma(gv[u][r], vr[r], acc);
+              rsv[p * CG + u] = acc;
+            }
+          }
+          fx_reduce_scatter(rsv);
+          const int q = lane >> 1, col = jb + (q >> 3) * CG * NW + (q & 7);
+          if ((lane & 1) == 0 && col < n) LV(vout + col) = (vadd >= 0) ? rsv[0] + LV(vadd + col) : rsv[0];
+        }
+        BAR();
+        LSTAMP(NSTAMP + 1 + 5);
+        return;
+      }
+#endif
       for (int j0 = CG * wv; j0 < n; j0 += CG * NW) {
         gcdbl* g0 = Gp + (int64_t)j0 * k;
         const int nl = n - j0;
