@@ -46,6 +46,9 @@
 #ifndef SOCP_LG_SYRK_SYNC
 #define SOCP_LG_SYRK_SYNC 128  // form_H: rows of k between workgroup barriers (0: none)
 #endif
+#ifndef SOCP_LG_SYRK_PIPE
+#define SOCP_LG_SYRK_PIPE 0  // form_H: 8-row k-steps with the next step's operands loaded ahead (0: 16-row steps)
+#endif
 #ifndef SOCP_LG_GT_RS
 #define SOCP_LG_GT_RS 0  // gemv_Gt: four passes' 32 column sums by one reduce-scatter (0: per-column all-reduces)
 #endif
@@ -740,6 +743,41 @@ struct Large {
     }
   }
 
+  // The SYRK's block product with its operands one step ahead: k-steps of 8
+  // rows (lane group g feeds rows k0 + 2g + s of MFMA s = 0, 1: one 16-byte
+  // load per tile and lane), the next step's loads issued before this step's
+  // 32 MFMAs from a second register buffer -- the same registers as
+  // blk_gemm's one 16-row buffer.  kr a multiple of 16.
+  template <bool LO = false>
+  __device__ __forceinline__ void blk_gemm_pipe(d4 (&acc)[4][4], gcdbl* P, int ld, int I0, int J0, int kr,
+                                                bool same) {
+    const int g = lane >> 4, cl = lane & 15;
+    dbl2 a0[4], b0[4], a1[4], b1[4];
+    auto load = [&](dbl2 (&a)[4], dbl2 (&b)[4], int k0) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a[t] = *reinterpret_cast<gcdbl2*>(P + (int64_t)(I0 + 16 * t + cl) * ld + k0 + 2 * g);
+        b[t] = same ? a[t] : *reinterpret_cast<gcdbl2*>(P + (int64_t)(J0 + 16 * t + cl) * ld + k0 + 2 * g);
+      }
+    };
+    auto mm = [&](const dbl2 (&a)[4], const dbl2 (&b)[4]) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+          for (int tb = 0; tb < 4; ++tb)
+            if (!LO || tb <= ta) acc[ta][tb] = mfma(a[ta][s], b[tb][s], acc[ta][tb]);
+    };
+    load(a0, b0, 0);
+    for (int k0 = 0; k0 < kr; k0 += 16) {
+      load(a1, b1, k0 + 8);
+      mm(a0, b0);
+      if (k0 + 16 < kr) load(a0, b0, k0 + 16);
+      mm(a1, b1);
+    }
+  }
+
   // The sweep's deferred Gram update, acc += sum_{c<64} Y[c][I-slice]' (fv[c]
   // Y[c][J-slice]) for the row-major 64-row panel Y (row c at Y + c*ld), in the
   // transposed MFMA orientation: acc[a][b] (lane (g, cl),
@@ -1308,10 +1346,17 @@ struct Large {
         for (int k0 = 0; k0 < KP; k0 += KB) {
           const int kr = KP - k0 < KB ? KP - k0 : KB;
           if (t < nblk) {
+#if SOCP_LG_SYRK_PIPE
+            if (I == J)
+              blk_gemm_pipe<true>(acc, Xw + k0, KP, 64 * I, 64 * J, kr, true);
+            else
+              blk_gemm_pipe(acc, Xw + k0, KP, 64 * I, 64 * J, kr, false);
+#else
             if (I == J)
               blk_gemm<true>(acc, Xw + k0, Xw + k0, KP, 64 * I, 64 * J, kr, true, -1);
             else
               blk_gemm(acc, Xw + k0, Xw + k0, KP, 64 * I, 64 * J, kr, false, -1);
+#endif
           }
           __builtin_amdgcn_s_barrier();
         }
