@@ -1306,12 +1306,26 @@ struct Large {
   // per block; padding diagonal = 1.
   __device__ __forceinline__ static int syrk_order8(int t) {
     // (I << 3) | J of the t-th block, rounds of eight (form_H)
+#if SOCP_LG_SYRK_ORDER == 2
+    // also balanced over the SIMDs (wavefronts w and w + 4 share one): the
+    // diagonal blocks (10 of 16 tiles) of rounds 1 and 2 on wavefronts 0-3
+    // beside an off-diagonal block each, the last round's four blocks on
+    // wavefronts 0-3 -- every SIMD issues the same MFMAs between barriers
+    // (132 tile-steps per k-step in all, the 528 / 4 minimum; 26 panel reads)
+    constexpr unsigned char tab[36] = {
+        0x00, 0x09, 0x12, 0x1b, 0x08, 0x10, 0x11, 0x18,  // panels 0..3: diagonal, off-diagonal
+        0x24, 0x2d, 0x36, 0x3f, 0x2c, 0x34, 0x35, 0x3c,  // panels 4..7
+        0x20, 0x21, 0x22, 0x23, 0x28, 0x29, 0x2a, 0x2b,  // {4,5} x {0..3}
+        0x30, 0x31, 0x32, 0x33, 0x38, 0x39, 0x3a, 0x3b,  // {6,7} x {0..3}
+        0x19, 0x1a, 0x3d, 0x3e};                         // (3,1) (3,2) (7,5) (7,6)
+#else
     constexpr unsigned char tab[36] = {
         0x00, 0x08, 0x09, 0x10, 0x11, 0x12, 0x18, 0x19,  // panels 0..3
         0x24, 0x2c, 0x2d, 0x34, 0x35, 0x36, 0x3c, 0x3d,  // panels 4..7
         0x20, 0x21, 0x22, 0x23, 0x28, 0x29, 0x2a, 0x2b,  // {4,5} x {0..3}
         0x30, 0x31, 0x32, 0x33, 0x38, 0x39, 0x3a, 0x3b,  // {6,7} x {0..3}
         0x1a, 0x1b, 0x3e, 0x3f};                         // (3,2) (3,3) (7,6) (7,7)
+#endif
     return tab[t];
   }
   __device__ void form_H(bool addAA) {
