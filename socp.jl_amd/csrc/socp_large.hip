@@ -46,12 +46,6 @@
 #ifndef SOCP_LG_SYRK_SYNC
 #define SOCP_LG_SYRK_SYNC 128  // form_H: rows of k between workgroup barriers (0: none)
 #endif
-#ifndef SOCP_LG_SYRK_PIPE
-#define SOCP_LG_SYRK_PIPE 0  // form_H: 8-row k-steps with the next step's operands loaded ahead (0: 16-row steps)
-#endif
-#ifndef SOCP_LG_GT_RS
-#define SOCP_LG_GT_RS 0  // gemv_Gt: four passes' 32 column sums by one reduce-scatter (0: per-column all-reduces)
-#endif
 #ifndef SOCP_LG_FX_RS
 #define SOCP_LG_FX_RS 1  // W^-1 G: the 32 cone sums of a pass by one reduce-scatter (0: 32 all-reduces)
 #endif
@@ -60,12 +54,6 @@
 #endif
 #ifndef SOCP_LG_SYRK_ORDER
 #define SOCP_LG_SYRK_ORDER 1  // form_H with SYRK_SYNC at NPAD = 512: the panel-sharing round order (0: row-major)
-#endif
-#ifndef SOCP_LG_ZU_SYNC
-#define SOCP_LG_ZU_SYNC 0  // chol_fwd_multi: rows of L between workgroup barriers (0: none)
-#endif
-#ifndef SOCP_LG_CATCH_SYNC
-#define SOCP_LG_CATCH_SYNC 0  // chol_nb's catch-up: panels between workgroup barriers (0: none)
 #endif
 #ifndef SOCP_LG_SYRK_UNROLL
 #define SOCP_LG_SYRK_UNROLL 1  // blk_gemm's k loop (16 rows per step)
@@ -743,41 +731,6 @@ struct Large {
     }
   }
 
-  // The SYRK's block product with its operands one step ahead: k-steps of 8
-  // rows (lane group g feeds rows k0 + 2g + s of MFMA s = 0, 1: one 16-byte
-  // load per tile and lane), the next step's loads issued before this step's
-  // 32 MFMAs from a second register buffer -- the same registers as
-  // blk_gemm's one 16-row buffer.  kr a multiple of 16.
-  template <bool LO = false>
-  __device__ __forceinline__ void blk_gemm_pipe(d4 (&acc)[4][4], gcdbl* P, int ld, int I0, int J0, int kr,
-                                                bool same) {
-    const int g = lane >> 4, cl = lane & 15;
-    dbl2 a0[4], b0[4], a1[4], b1[4];
-    auto load = [&](dbl2 (&a)[4], dbl2 (&b)[4], int k0) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        a[t] = *reinterpret_cast<gcdbl2*>(P + (int64_t)(I0 + 16 * t + cl) * ld + k0 + 2 * g);
-        b[t] = same ? a[t] : *reinterpret_cast<gcdbl2*>(P + (int64_t)(J0 + 16 * t + cl) * ld + k0 + 2 * g);
-      }
-    };
-    auto mm = [&](const dbl2 (&a)[4], const dbl2 (&b)[4]) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int ta = 0; ta < 4; ++ta)
-#pragma unroll
-          for (int tb = 0; tb < 4; ++tb)
-            if (!LO || tb <= ta) acc[ta][tb] = mfma(a[ta][s], b[tb][s], acc[ta][tb]);
-    };
-    load(a0, b0, 0);
-    for (int k0 = 0; k0 < kr; k0 += 16) {
-      load(a1, b1, k0 + 8);
-      mm(a0, b0);
-      if (k0 + 16 < kr) load(a0, b0, k0 + 16);
-      mm(a1, b1);
-    }
-  }
-
   // The sweep's deferred Gram update, acc += sum_{c<64} Y[c][I-slice]' (fv[c]
   // Y[c][J-slice]) for the row-major 64-row panel Y (row c at Y + c*ld), in the
   // transposed MFMA orientation: acc[a][b] (lane (g, cl),
@@ -1360,17 +1313,10 @@ struct Large {
         for (int k0 = 0; k0 < KP; k0 += KB) {
           const int kr = KP - k0 < KB ? KP - k0 : KB;
           if (t < nblk) {
-#if SOCP_LG_SYRK_PIPE
-            if (I == J)
-              blk_gemm_pipe<true>(acc, Xw + k0, KP, 64 * I, 64 * J, kr, true);
-            else
-              blk_gemm_pipe(acc, Xw + k0, KP, 64 * I, 64 * J, kr, false);
-#else
             if (I == J)
               blk_gemm<true>(acc, Xw + k0, Xw + k0, KP, 64 * I, 64 * J, kr, true, -1);
             else
               blk_gemm(acc, Xw + k0, Xw + k0, KP, 64 * I, 64 * J, kr, false, -1);
-#endif
           }
           __builtin_amdgcn_s_barrier();
         }
@@ -1605,36 +1551,6 @@ struct Large {
       if (P > 0 && SOCP_LG_CATCH_SPLIT && SOCP_LG_CATCH_SPLIT_K * (nb - P) <= NW) {
         // few blocks left: each block's catch-up split into its four 16-column
         // groups, one per wavefront (bitwise the whole-block result)
-#if SOCP_LG_CATCH_SYNC > 0
-        if (4 * (nb - P) <= NW) {
-          // one item per wavefront: the items share panel Q's rows, read in
-          // step (see the whole-block case below)
-          const int it = wv, t = P + it / 4, a_ = it % 4;
-          const bool act = it < 4 * (nb - P);
-          d4 acc[4];
-          if (act) {
-            if (t == P)
-              load_colT<true>(acc, M, ld, 64 * t, 64 * P, a_);
-            else
-              load_colT(acc, M, ld, 64 * t, 64 * P, a_);
-          }
-          for (int Q = 0; Q < P; ++Q) {
-            if (act) {
-              if (t == P)
-                gram_colT<true>(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q, a_);
-              else
-                gram_colT(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q, a_);
-            }
-            if ((Q + 1) % SOCP_LG_CATCH_SYNC == 0) __builtin_amdgcn_s_barrier();
-          }
-          if (act) {
-            if (t == P)
-              store_colT<true>(acc, M, ld, 64 * t, 64 * P, a_);
-            else
-              store_colT(acc, M, ld, 64 * t, 64 * P, a_);
-          }
-        } else
-#endif
         for (int it = wv; it < 4 * (nb - P); it += NW) {
           const int t = P + it / 4, a_ = it % 4;
           d4 acc[4];
@@ -1650,38 +1566,6 @@ struct Large {
         }
         BAR();
       } else if (P > 0) {
-#if SOCP_LG_CATCH_SYNC > 0
-        if (nb - P <= NW) {
-          // one block per wavefront, and every block reads panel Q's rows of
-          // the P block: with the wavefronts in step (a barrier every
-          // SOCP_LG_CATCH_SYNC panels) those rows come from L2 after the
-          // first reader
-          const int t = P + wv;
-          const bool act = t < nb;
-          d4 acc[4][4];
-          if (act) {
-            if (t == P)
-              load_blkT<true>(acc, M, ld, 64 * t, 64 * P);
-            else
-              load_blkT(acc, M, ld, 64 * t, 64 * P);
-          }
-          for (int Q = 0; Q < P; ++Q) {
-            if (act) {
-              if (t == P)
-                gram_blkT<true>(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q);
-              else
-                gram_blkT(acc, M + (int64_t)64 * Q * ld, ld, 64 * t, 64 * P, Rv + 64 * Q);
-            }
-            if ((Q + 1) % SOCP_LG_CATCH_SYNC == 0) __builtin_amdgcn_s_barrier();
-          }
-          if (act) {
-            if (t == P)
-              store_blkT<true>(acc, M, ld, 64 * t, 64 * P);
-            else
-              store_blkT(acc, M, ld, 64 * t, 64 * P);
-          }
-        } else
-#endif
         for (int t = P + wv; t < nb; t += NW) {
           d4 acc[4][4];
           if (t == P) {
@@ -1873,10 +1757,6 @@ struct Large {
     const int NB = L.NPAD / 64, MT = L.MPAD / 16, MP = L.MPAD;
     gdbl* const Rs = Yp;
     const d4 zero = {0.0, 0.0, 0.0, 0.0};
-    // SOCP_LG_ZU_SYNC: when every wavefront has the same number of tiles, a
-    // workgroup barrier every SOCP_LG_ZU_SYNC rows keeps the tiles that share
-    // rows of L (same ta) or of Z (same tb) in step, so they meet in L2
-    const bool zsync = SOCP_LG_ZU_SYNC > 0 && (4 * MT) % NW == 0;
     for (int P = 0; P < NB; ++P) {
       const int P0 = 64 * P;
       for (int tt = wv; tt < 4 * MT; tt += NW) {
@@ -1889,8 +1769,6 @@ struct Large {
         // memory round trip per 32 rows instead of per 8); acc0 / acc1 take the
         // same rows in the same order as before
         for (int y0 = 0; y0 < P0; y0 += 4 * SOCP_LG_ZU) {
-          if (SOCP_LG_ZU_SYNC > 0 && zsync && y0 > 0 && y0 % (SOCP_LG_ZU_SYNC > 0 ? SOCP_LG_ZU_SYNC : 1) == 0)
-            __builtin_amdgcn_s_barrier();
           double a[SOCP_LG_ZU], b[SOCP_LG_ZU];
 #pragma unroll
           for (int u = 0; u < SOCP_LG_ZU; ++u) {
@@ -2357,46 +2235,6 @@ struct Large {
       double vr[GT_R];
 #pragma unroll
       for (int r = 0; r < GT_R; ++r) vr[r] = (lane + 64 * r < k) ? LV(vin + lane + 64 * r) : 0.0;
-#if SOCP_LG_GT_RS
-      if constexpr (CG == 8) {
-        // four passes' column sums (32) reduced at once by fx_reduce_scatter
-        for (int jb = CG * wv; jb < n; jb += 4 * CG * NW) {
-          double rsv[32];
-#pragma unroll
-          for (int p = 0; p < 4; ++p) {
-            const int j0 = jb + p * CG * NW;
-            if (j0 >= n) {  // wave-uniform
-#pragma unroll
-              for (int u = 0; u < CG; ++u) rsv[p * CG + u] = 0.0;
-              continue;
-            }
-            gcdbl* g0 = Gp + (int64_t)j0 * k;
-            const int nl = n - j0;
-            double gv[CG][GT_R];
-#pragma unroll
-            for (int u = 0; u < CG; ++u)
-#pragma unroll
-              for (int r = 0; r < GT_R; ++r) {
-                const int row = lane + 64 * r;
-                gv[u][r] = (row < k) ? g0[(int64_t)(u < nl ? u : 0) * k + row] : 0.0;
-              }
-#pragma unroll
-            for (int u = 0; u < CG; ++u) {
-              double acc = 0.0;
-#pragma unroll
-              for (int r = 0; r < GT_R; ++r) acc = fma(gv[u][r], vr[r], acc);
-              rsv[p * CG + u] = acc;
-            }
-          }
-          fx_reduce_scatter(rsv);
-          const int q = lane >> 1, col = jb + (q >> 3) * CG * NW + (q & 7);
-          if ((lane & 1) == 0 && col < n) LV(vout + col) = (vadd >= 0) ? rsv[0] + LV(vadd + col) : rsv[0];
-        }
-        BAR();
-        LSTAMP(NSTAMP + 1 + 5);
-        return;
-      }
-#endif
       for (int j0 = CG * wv; j0 < n; j0 += CG * NW) {
         gcdbl* g0 = Gp + (int64_t)j0 * k;
         const int nl = n - j0;

@@ -223,9 +223,6 @@ __device__ __forceinline__ double dot_strided(const double* p, int64_t stride, c
 #define SQR_GU 16
 #endif
 
-#ifndef SQR_CHOL_LDS
-#define SQR_CHOL_LDS 0  // the register Cholesky's column broadcasts through the LDS (0: readlanes)
-#endif
 #ifndef SQR_S_MFMA
 #define SQR_S_MFMA 1  // 0: S = C'C one entry per lane (dot products out of LDS)
 #endif
@@ -526,9 +523,6 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
       if (lane >= n) h[l] = lane == l ? 1.0 : 0.0;
     SQ_STAMP(1);
     // ---- Cholesky, right-looking, in registers
-#if SQR_CHOL_LDS
-    double* colb = lds + L.o_X;  // the transpose's staging is free now (16-byte aligned)
-#endif
     bool badc = false;  // a pivot <= 0 or NaN: the rest runs on NaNs, the status says so
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
@@ -544,22 +538,8 @@ __device__ __forceinline__ void setup_problem(Ctx& C, int64_t p) {
       } else {
         h[j] = 0.0;
       }
-#if SQR_CHOL_LDS
-      // column j of L to the LDS once, read back as broadcasts two entries at
-      // a time (the same products as the readlane form: bitwise equal)
-      colb[lane] = h[j];
-      wsync();
-#pragma unroll
-      for (int l = (j + 1) & ~1; l < NC; l += 2) {
-        const double2 v = *reinterpret_cast<const double2*>(colb + l);
-        if (l > j) h[l] -= h[j] * v.x;
-        h[l + 1] -= h[j] * v.y;
-      }
-      wsync();  // the next column's writes after every read of this one
-#else
 #pragma unroll
       for (int l = j + 1; l < NC; ++l) h[l] -= h[j] * bcast(h[j], l);
-#endif
       __builtin_amdgcn_sched_barrier(0);  // bounds the live ranges of straight-line code
     }
     if (badc) status = SQR_CHOL_H;
