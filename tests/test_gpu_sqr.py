@@ -476,6 +476,29 @@ def test_sqr_solve_socp_trajectory(oracle, cfg, K):
             assert e <= 1e-8, (p, key, e)
 
 
+@pytest.mark.parametrize("case", ["sing", "m0"])
+def test_sqr_solve_socp_trajectory_sing_and_m0(oracle, case):
+    """The wave kernels' whole-IPM path (the setup kernel's fused residuals,
+    SqrArgs::fuse_resid) with `sing` problems (H = G'DG + A'A, m0 = dy - cy;
+    every other problem of the batch) and with no equality constraints (m = 0):
+    fixed-K trajectories vs the oracle's F_SQR IPM, rel <= 1e-8, equal status
+    and iteration counts."""
+    cfg, B, K = C1, 16, 3
+    m = 0 if case == "m0" else cfg.m
+    d = oracle.generate(cfg.cones, B, cfg.n, m, cfg.k, cfg.seed + 7)
+    sing = (np.arange(B) % 2).astype(np.uint8) if case == "sing" else np.zeros(B, np.uint8)
+    r = oracle.batch_solve(cfg.cones, cfg.n, m, cfg.k, d["c"], d["A"], d["b"], d["G"], d["h"], sing=sing,
+                           params=oracle.Params(maxit=K, tol=0.0, flags=oracle.F_SQR))
+    hd = S.SqrHandle(cfg.cones, cfg.n, m, cfg.k, d["A"], d["G"], sing)
+    g = hd.solve_socp(d["c"], d["b"], d["h"], maxit=K, tol=0.0)
+    assert (g["status"] == r["status"]).all() and (g["iters"] == r["iters"]).all()
+    for p in range(B):
+        for key, L in (("x", cfg.n), ("z", cfg.k), ("s", cfg.k)):
+            a_, b_ = g[key][p * L:(p + 1) * L], r[key][p * L:(p + 1) * L]
+            e = np.linalg.norm(a_ - b_) / np.linalg.norm(b_)
+            assert e <= 1e-8, (p, key, e)
+
+
 def test_sqr_solve_socp_reference_rule_outcomes(oracle):
     """The reference stopping rule (tol = 1e-5 absolute, maxit = 40) on 256 C2
     problems: outcome statistics of the HIP rank-update IPM vs the oracle's
