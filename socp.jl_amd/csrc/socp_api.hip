@@ -1081,6 +1081,9 @@ extern "C" int socp_sqr_solve_kkt(socp_sqr* h, const double* dx, const double* d
 #ifndef SQR_FUSE_RESID
 #define SQR_FUSE_RESID 1  // 0: the separate residual kernel after every setup launch (A/B builds)
 #endif
+#ifndef SQR_FUSE_SOLVES
+#define SQR_FUSE_SOLVES 1  // the iteration's two solves and step phases in one launch (0: four launches)
+#endif
 extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b, const double* hv,
                                    const socp_params* params, double* x, double* y, double* z, double* s,
                                    int32_t* iters, int32_t* status, double* res) {
@@ -1182,13 +1185,34 @@ extern "C" int socp_sqr_solve_socp(socp_sqr* h, const double* c, const double* b
     su.ostatus = ia.status; su.oactive = ia.active; su.n_active = ia.n_active;
     su.tol = P.tol;
   }
+  // the wave shapes run the two solves and both step phases in one launch
+  const void* solves = SQR_FUSE_SOLVES ? sqr_ipm_solves_kernel_ptr(n, m) : nullptr;
+  size_t solves_lds = 0;
+  if (solves) {
+    const SqrLayout Ls = sqr_solve_layout(n, m, k, h->a.nc);
+    solves_lds = (size_t)Ls.total * sizeof(double);
+    if (lds > solves_lds) solves_lds = lds;
+    if (solves_lds > 160 * 1024) {
+      solves = nullptr;
+    } else if (solves_lds > 64 * 1024) {
+      HIPCHK(hipFuncSetAttribute(solves, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solves_lds));
+    }
+  }
   for (int it = 0; it < P.maxit; ++it) {
     TRY(sqr_launch(h, su, true, false));   // compute_scaling + setup_iter (+ fused: the residuals)
     if (!fuse) TRY(ipm(2, it));            // residuals, exit test, affine right-hand side
-    TRY(sqr_launch(h, sv, false, false));  // solve_kkt (affine)
-    TRY(ipm(3, it));                       // step, sigma, mu, corrector right-hand side
-    TRY(sqr_launch(h, sv, false, false));  // solve_kkt (combined)
-    TRY(ipm(4, it));                // step and update
+    if (solves) {
+      SqrArgs sl = sv;
+      sl.stamps = g_stamps;
+      int itv = it;
+      void* fargs[] = {&sl, &ia, &itv};
+      HIPCHK(hipLaunchKernel(solves, grid, blk, fargs, solves_lds, ctx->stream));
+    } else {
+      TRY(sqr_launch(h, sv, false, false));  // solve_kkt (affine)
+      TRY(ipm(3, it));                       // step, sigma, mu, corrector right-hand side
+      TRY(sqr_launch(h, sv, false, false));  // solve_kkt (combined)
+      TRY(ipm(4, it));                       // step and update
+    }
     // under a stopping rule, look every 4 iterations whether any problem is
     // still iterating: the launches over an all-stopped batch are skipped
     if (P.tol > 0.0 && (it & 3) == 3 && it + 1 < P.maxit) {

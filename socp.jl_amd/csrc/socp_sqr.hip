@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include "socp_sqr.hpp"
+#include "socp_sqr_step.hpp"
 
 namespace socp {
 
@@ -1295,6 +1296,39 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC >= 64 ? S
   solve_problem<NC>(C, (int64_t)blockIdx.x);
 }
 
+// socp_sqr_solve_socp's iteration after setup_iter (solver.jl:127-150) in one
+// launch: solve_kkt (affine), step1, solve_kkt (combined), step2 for one
+// problem per wavefront.  The same device code as the four launches it
+// replaces, so the iterates are bitwise theirs; the second solve's passes over
+// G and the factor record follow the first within microseconds (L2 / MALL
+// instead of HBM), and three launches and their record reloads go.
+__device__ __forceinline__ void global_rw_fence() {
+  // this wavefront's global stores visible to its own later loads from other
+  // lanes: workgroup scope (one CU's write-through L1; an agent-scope fence
+  // would write back and invalidate the XCD's L2 per problem)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
+template <int NC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NC >= 64 ? SQR_SOLVE_WPE : 3))) void
+socp_sqr_ipm_solves_kernel(SqrArgs a, SqrIpmArgs ia, int it) {
+  extern __shared__ double lds_dyn[];
+  const int64_t p = blockIdx.x;
+  if (!ia.active[p]) return;
+  const int lane = (int)threadIdx.x;
+  const SqrLayout L = sqr_solve_layout(a.n, a.m, a.k, a.nc);
+  Ctx C{a, L, lds_dyn, lane};
+  solve_problem<NC>(C, p);  // affine (solver.jl:127)
+  global_rw_fence();
+  wsync();
+  if (!ipm_step1_problem(ia, p, lds_dyn, lane)) return;
+  global_rw_fence();
+  wsync();
+  solve_problem<NC>(C, p);  // combined (:141)
+  global_rw_fence();
+  wsync();
+  ipm_step2_problem(ia, p, it, lds_dyn, lane);
+}
+
 __global__ __launch_bounds__(SQR_LT) void socp_sqr_setup_wg_kernel(SqrArgs a) {
   extern __shared__ double lds_dyn[];
   const SqrLayout L = sqr_layout(a.n, a.m, a.k, a.nc);
@@ -1318,6 +1352,13 @@ const void* sqr_setup_kernel_ptr(int n, int m) {
   if (n <= 32) return (const void*)socp_sqr_setup_kernel<32>;
   if (n <= 48) return (const void*)socp_sqr_setup_kernel<48>;
   return (const void*)socp_sqr_setup_kernel<64>;
+}
+const void* sqr_ipm_solves_kernel_ptr(int n, int m) {
+  if (n > SQR_NMAX || m > SQR_NMAX) return nullptr;
+  if (n <= 16) return (const void*)socp_sqr_ipm_solves_kernel<16>;
+  if (n <= 32) return (const void*)socp_sqr_ipm_solves_kernel<32>;
+  if (n <= 48) return (const void*)socp_sqr_ipm_solves_kernel<48>;
+  return (const void*)socp_sqr_ipm_solves_kernel<64>;
 }
 const void* sqr_solve_kernel_ptr(int n, int m) {
   if (n > SQR_NMAX || m > SQR_NMAX) return (const void*)socp_sqr_solve_wg_kernel;

@@ -172,6 +172,10 @@ const void* sqr_ipm_kernel_ptr(int which);
 // 16), workgroup kernels (SQR_LT threads) above
 const void* sqr_setup_kernel_ptr(int n, int m);
 const void* sqr_solve_kernel_ptr(int n, int m);
+// socp_sqr_solve_socp's two solves of an iteration with their step phases in
+// one launch (wave shapes; nullptr for the workgroup shapes):
+// kernel(SqrArgs solve, SqrIpmArgs ipm, int it)
+const void* sqr_ipm_solves_kernel_ptr(int n, int m);
 inline int sqr_block_threads(int n, int m) { return (n > SQR_NMAX || m > SQR_NMAX) ? SQR_LT : 64; }
 
 }  // namespace socp
