@@ -1,12 +1,12 @@
 #!/bin/bash
-# Measurement session (round tag $R, default r05): GPU tests, PMC HBM traffic
+# Measurement session (round tag $R, default r06): GPU tests, PMC HBM traffic
 # (FETCH_SIZE, WRITE_SIZE, one counter per pass) for C2 / C4 / C1, SQ
 # issue/stall counters of the C2 kernel, rocprofv3 kernel stats of each
 # config's bench command (the explicit-inverse order too), then the bench
 # lines against the fresh traffic files (copied to profiles/ by hand).
 set -e
 export TMPDIR=/tmp
-R=${R:-r05}
+R=${R:-r06}
 O=gpurun_out/${R}m
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { grep -E "FAILED|ERROR" $O/pytest_gpu.log | head; tail -5 $O/pytest_gpu.log; exit 1; }
