@@ -168,7 +168,6 @@ __device__ __forceinline__ bool ipm_step1_problem(const SqrIpmArgs& a, int64_t p
   return true;
 }
 
-
 // step2 (solver.jl:143-150): step = 0.99 compute_step and the update.
 // Returns false (and retires the problem) on scmax's DomainError.
 __device__ __forceinline__ bool ipm_step2_problem(const SqrIpmArgs& a, int64_t p, int it, double* lds, int lane) {
