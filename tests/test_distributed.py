@@ -328,6 +328,33 @@ def test_bench_one_gpu_line_unchanged_shape():
     assert line["config"]["parallelism"].startswith("dp1")
 
 
+def test_bench_line_carries_the_driver_contract():
+    """The one JSON line keeps every key the driver and the judge read: the
+    metric / value / unit / n_gpus / steps / warmup / ms_per_step block, the
+    config naming the workload, roofline (bound, achieved, peak, unit, frac,
+    traffic) and cpu_baseline (null at --no-cpu).  Stub solve, CPU only."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--batch", "32", "--stub-solve", "--no-cpu"],
+                       capture_output=True, text=True, timeout=300, env=_bench_env(), cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _bench_json(r.stdout)
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert key in line, key
+    assert line["unit"] == "problem-iterations/s" and line["higher_is_better"] is True
+    assert line["scaling"] == "weak" and line["dtype"] == "f64" and line["vs_baseline"] is None
+    assert line["steps"] == 2 and line["warmup"] == 1 and line["n_gpus"] == 1
+    assert {"workload", "global_batch", "parallelism"} <= set(line["config"])
+    roof = line["roofline"]
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(roof)
+    assert roof["bound"] in ("hbm", "mfma") and roof["unit"] in ("GB/s", "TFLOP/s")
+    assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) <= 1e-12 * max(1.0, roof["frac"])
+    assert line["cpu_baseline"] is None
+
+
 def test_bench_world_size_mismatch_fails():
     """Under a launcher, WORLD_SIZE must equal --gpus: a mismatch exits non-zero
     before any process group or device is touched."""
